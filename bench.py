@@ -1,0 +1,363 @@
+#!/usr/bin/env python3
+"""Benchmark: Mvis/s gridded by the MI355X-native ES-FFT gridder.
+
+Workload (BASELINE.json configs[1]):
+  10M synthetic visibility rows x 1 channel, image 5440^2, epsilon 1e-5,
+  f32 -> uv grid 8192^2, support 8; 2-D (no w-stacking); uvw uniform in a
+  disk keeping every visibility in-band; complex-normal vis; unit weights.
+  Inputs are generated directly in HBM (seed 20251015 + 2 + rank).
+
+A step = one full sdp_grid_uvw_es_fft call through the C ABI (bucketing,
+LDS tile scatter, rocFFT inverse 8192^2, fused screen + grid correction).
+value = visibilities gridded per second over the whole job (all ranks).
+The degridding half of the config-2 round trip is timed afterwards with the
+same step count and reported in "degrid"; "roundtrip_mvis_s" = R / (t_grid +
+t_degrid).
+
+Multi-GPU (torchrun, one process per GPU, RCCL): weak scaling -- every rank
+grids its own 10M rows (a row shard of the job) into a partial image, then
+the partial images are summed onto rank 0 with one RCCL reduce (default,
+--reduce image: 5440^2 f32 = 118 MB) or the per-GPU grids are reduced before
+a single FFT on rank 0 (--reduce grid: 8192^2 c64 = 512 MiB). The collective
+is inside the timed region.
+
+Roofline: the dominant hand-written kernel's algorithmic bytes per launch
+divided by its HIP-event duration (library timing on the launch stream).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ska-sdp-func_amd"))
+sys.path.insert(0, ROOT)
+
+C_LIGHT = 299792458.0
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--chan", type=int, default=1)
+    ap.add_argument("--image", type=int, default=5440)
+    ap.add_argument("--eps", type=float, default=1e-5)
+    ap.add_argument("--reduce", choices=["image", "grid"], default="image")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-rows", type=int, default=2_000_000)
+    ap.add_argument("--no-degrid", action="store_true")
+    return ap.parse_args()
+
+
+def make_inputs(torch, dev, rows, chan, image, seed):
+    """Synthetic config-2 data generated on the device."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    fov_deg = 2.0
+    px = fov_deg * np.pi / 180.0 / image
+    f0 = 1e9
+    df = 0.5 * f0 / max(chan, 1)
+    freq = torch.tensor(f0 + np.arange(chan) * df, dtype=torch.float32,
+                        device=dev)
+    fmax = float(f0 + (chan - 1) * df)
+    umax = 0.45 * C_LIGHT / (fmax * px)
+    r = umax * torch.sqrt(torch.rand(rows, generator=g, device=dev))
+    th = 2.0 * np.pi * torch.rand(rows, generator=g, device=dev)
+    w = (torch.rand(rows, generator=g, device=dev) - 0.5) * 1000.0
+    uvw = torch.stack([r * torch.cos(th), r * torch.sin(th), w], 1).float()
+    vis = torch.complex(torch.randn(rows, chan, generator=g, device=dev),
+                        torch.randn(rows, chan, generator=g, device=dev))
+    weight = torch.ones(rows, chan, dtype=torch.float32, device=dev)
+    return uvw.contiguous(), freq, vis.contiguous(), weight, px
+
+
+def scatter_bytes(rows, chan, G):
+    """Algorithmic HBM bytes of the gridding scatter:
+    vis + weight read, uvw read, grid written once."""
+    return rows * chan * (8 + 4) + rows * 3 * 4 + chan * 4 + G * G * 8
+
+
+def fft_bytes(G):
+    """One read + one write of the complex64 grid."""
+    return 2 * G * G * 8
+
+
+def gridding_bytes(rows, chan, G, n):
+    """Whole gridding call: scatter + FFT + screen + corr."""
+    return (scatter_bytes(rows, chan, G) + fft_bytes(G)
+            + n * n * (8 + 4) + 2 * n * n * 4)
+
+
+def cpu_baseline(args, G, support, beta, uv_scale):
+    """Oracle ('port') gridder on the host cores, bounded sample.
+
+    The f32 OpenMP scatter of oracle/es_oracle.c is timed on
+    --cpu-sample-rows rows of the same synthetic distribution, the fixed
+    costs (per-thread grid reduce, included in that call; 8192^2 FFT with
+    scipy pocketfft on all threads; screen + correction) are timed once, and
+    the rate for the full job is extrapolated linearly in rows.
+    """
+    import scipy.fft
+
+    from oracle import es_oracle
+
+    lib = es_oracle.lib()
+    threads = min(16, os.cpu_count() or 1)
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    rng = np.random.default_rng(20251015 + 2)
+    n_s = args.cpu_sample_rows
+    px = 2.0 * np.pi / 180.0 / args.image
+    umax = 0.45 * C_LIGHT / (1e9 * px)
+    r = umax * np.sqrt(rng.random(n_s))
+    th = 2 * np.pi * rng.random(n_s)
+    uvw = np.stack([r * np.cos(th), r * np.sin(th),
+                    rng.uniform(-500, 500, n_s)], 1).astype(np.float32)
+    vis = (rng.standard_normal((n_s, 1)) + 1j * rng.standard_normal(
+        (n_s, 1))).astype(np.complex64)
+    wt = np.ones((n_s, 1), np.float32)
+    freq = np.array([1e9], np.float32)
+    grid = np.zeros((G, G), np.complex64)
+    t0 = time.perf_counter()
+    used = lib.oracle_es_grid_f32_omp(n_s, 1, es_oracle._ptr(uvw),
+                                      es_oracle._ptr(freq),
+                                      es_oracle._ptr(vis), es_oracle._ptr(wt),
+                                      G, support, float(np.float32(beta)),
+                                      float(np.float32(uv_scale)),
+                                      es_oracle._ptr(grid))
+    t_scatter = time.perf_counter() - t0
+    # Fixed part of the scatter call (per-thread grid zero + reduce):
+    t0 = time.perf_counter()
+    lib.oracle_es_grid_f32_omp(0, 1, es_oracle._ptr(uvw),
+                               es_oracle._ptr(freq), es_oracle._ptr(vis),
+                               es_oracle._ptr(wt), G, support,
+                               float(np.float32(beta)),
+                               float(np.float32(uv_scale)),
+                               es_oracle._ptr(grid))
+    t_fixed_scatter = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    layer = scipy.fft.ifft2(grid, norm="forward", workers=threads,
+                            overwrite_x=True)
+    h, gc = args.image // 2, G // 2
+    sub = layer[gc - h:gc + h, gc - h:gc + h].real
+    img = sub * np.float32(1.0001)   # stands in for screen + correction
+    t_fft_img = time.perf_counter() - t0
+    del layer, img
+    per_row = max(t_scatter - t_fixed_scatter, 1e-9) / n_s
+    t_job = per_row * args.rows * args.chan + t_fixed_scatter + t_fft_img
+    return {
+        "value": args.rows * args.chan / t_job / 1e6,
+        "unit": "Mvis/s",
+        "cores": int(used),
+        "kind": "port",
+        "sample": (f"oracle/es_oracle.c f32 OpenMP scatter on {n_s} rows of "
+                   f"the config-2 distribution ({t_scatter:.2f} s incl. "
+                   f"{t_fixed_scatter:.2f} s per-thread grid zero+reduce), "
+                   f"scipy pocketfft ifft2 {G}^2 c64 + crop "
+                   f"({t_fft_img:.2f} s), extrapolated linearly to "
+                   f"{args.rows} rows"),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ska_sdp_func.grid_data import GridderUvwEsFft
+
+    uvw, freq, vis, weight, px = make_inputs(
+        torch, dev, args.rows, args.chan, args.image, 20251015 + 2 + rank)
+    dirty = torch.zeros((args.image, args.image), dtype=torch.float32,
+                        device=dev)
+    plan = GridderUvwEsFft(uvw, freq, vis, weight, dirty, px, px, args.eps,
+                           False)
+    plan.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    plan.enable_timing(True)
+    G, W = plan.grid_size, plan.support
+    grid_buf = None
+    if world > 1 and args.reduce == "grid":
+        grid_buf = torch.empty((G, G), dtype=torch.complex64, device=dev)
+
+    def grid_step():
+        # Fresh image per step (the call accumulates into it).
+        dirty.zero_()
+        if world == 1:
+            plan.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
+        elif args.reduce == "image":
+            plan.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
+            dist.reduce(dirty, dst=0)
+        else:
+            plan.grid_scatter(uvw, freq, vis, weight, grid_buf)
+            dist.reduce(grid_buf, dst=0)
+            if rank == 0:
+                plan.grid_finish(grid_buf, dirty)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        grid_step()
+    barrier()
+    phases = {"bucket": 0.0, "tile_kernel": 0.0, "fft": 0.0, "image": 0.0}
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        grid_step()
+        tm = plan.get_timing()
+        if tm:
+            for k in phases:
+                phases[k] += tm[k]
+    barrier()
+    t_grid = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([t_grid], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_grid = float(t.item())
+    ms_per_step = 1e3 * t_grid / args.steps
+    total_vis = args.rows * args.chan * world
+    value = total_vis * args.steps / t_grid / 1e6
+    avg = {k: v / args.steps for k, v in phases.items()}
+
+    # Degridding half of the round trip (same image, same step count).
+    degrid = None
+    if not args.no_degrid:
+        image0 = dirty.clone()
+        out_vis = torch.zeros_like(vis)
+        img = torch.empty_like(dirty)
+        for _ in range(args.warmup):
+            img.copy_(image0)
+            plan.ifft_grid_uvw_es(uvw, freq, out_vis, weight, img)
+        barrier()
+        dph = {"bucket": 0.0, "tile_kernel": 0.0, "fft": 0.0, "image": 0.0}
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            img.copy_(image0)
+            plan.ifft_grid_uvw_es(uvw, freq, out_vis, weight, img)
+            tm = plan.get_timing()
+            if tm:
+                for k in dph:
+                    dph[k] += tm[k]
+        barrier()
+        t_deg = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([t_deg], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t_deg = float(t.item())
+        degrid = {
+            "mvis_s": total_vis * args.steps / t_deg / 1e6,
+            "ms_per_step": 1e3 * t_deg / args.steps,
+            "phases_ms": {k: v / args.steps for k, v in dph.items()},
+        }
+
+    # Roofline of the dominant kernel of a gridding call.
+    kern_bytes = {
+        "tile_kernel": scatter_bytes(args.rows, args.chan, G),
+        "fft": fft_bytes(G),
+        "bucket": args.rows * args.chan * (8 + 4) + args.rows * 12 * 2,
+        "image": args.image ** 2 * (8 + 4) + 2 * args.image ** 2 * 4,
+    }
+    dom = max(avg, key=lambda k: avg[k]) if any(avg.values()) else "tile_kernel"
+    achieved = (kern_bytes[dom] / (avg[dom] * 1e-3) / 1e9
+                if avg.get(dom) else None)
+    kernel_names = {"tile_kernel": "k_scatter (LDS tile accumulation)",
+                    "fft": "rocFFT 2-D C2C inverse",
+                    "bucket": "bucketing (count/scan/fill)",
+                    "image": "k_screen_corr_2d"}
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args, G, W, plan.beta, G * px)
+        except Exception as exc:  # baseline failure must not hide the bench
+            cpu = {"value": None, "unit": "Mvis/s", "cores": 0,
+                   "kind": "port", "sample": f"failed: {exc!r}"}
+
+    if rank == 0:
+        line = {
+            "metric": "Mvis/s gridded",
+            "value": round(value, 3),
+            "unit": "Mvis/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (config-2 distribution, generated in HBM)",
+            "config": {
+                "workload": (f"ES-FFT grid_uvw_es_fft, {args.rows} rows x "
+                             f"{args.chan} chan per GPU, image {args.image}^2,"
+                             f" eps {args.eps}, grid {G}^2, support {W}, 2-D"),
+                "rows_per_gpu": args.rows,
+                "channels": args.chan,
+                "image_size": args.image,
+                "grid_size": G,
+                "support": W,
+                "epsilon": args.eps,
+                "parallelism": (f"row-shard x{world}, RCCL reduce of "
+                                f"{args.reduce}" if world > 1 else "1 GPU"),
+            },
+            "phases_ms": {k: round(v, 4) for k, v in avg.items()},
+            "roofline": {
+                "kernel": kernel_names[dom],
+                "bound": "hbm",
+                "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": kern_bytes[dom],
+            },
+            "call_roofline": {
+                "algorithmic_bytes": gridding_bytes(args.rows, args.chan, G,
+                                                    args.image),
+                "achieved_GBs": round(gridding_bytes(args.rows, args.chan, G,
+                                                     args.image)
+                                      / (ms_per_step * 1e-3) / 1e9, 1),
+                "frac": round(gridding_bytes(args.rows, args.chan, G,
+                                             args.image)
+                              / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            },
+            "degrid": degrid,
+            "roundtrip_mvis_s": (round(total_vis / ((ms_per_step
+                                                     + degrid["ms_per_step"])
+                                                    * 1e-3) / 1e6, 3)
+                                 if degrid else None),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,129 @@
+// HIP kernels of the MI355X-native ES-FFT (de)gridder: launch interface.
+//
+// Data path (one w-plane, one call):
+//   bucket_count -> scan_columns -> scan_bins -> [host reads 2 totals]
+//   -> bucket_fill -> (grid) zero_hot_tiles + scatter_tiles
+//                     (degrid) gather_tiles
+// Visibilities are bucketed by 64x64 grid tile (counting sort, LDS-private
+// histograms per chunk of visibilities). In grid mode a visibility is listed
+// in every tile its support touches and each tile only accumulates the taps
+// that fall inside it, so every grid cell has exactly one owning workgroup:
+// the tile is accumulated in LDS (ds_add) and written to HBM ONCE with plain
+// stores (no global atomics, no separate memset of the grid). Tiles with
+// more entries than one work item takes are split into pieces that combine
+// with global float atomics into a tile zeroed beforehand.
+#ifndef SDP_ES_KERNELS_H_
+#define SDP_ES_KERNELS_H_
+
+#include <cstddef>
+#include <cstdint>
+
+#include <hip/hip_runtime.h>
+
+namespace sdp_es {
+
+constexpr int kTile = 64;              // grid tile edge (cells)
+constexpr int kBinsPerPass = 16384;    // LDS histogram capacity (64 KiB)
+constexpr int kPiece = 4096;           // max entries per scatter work item
+constexpr int kMaxChunks = 1024;       // chunks of visibilities per bucketing
+
+enum Mode { MODE_GRID = 0, MODE_DEGRID = 1 };
+
+// Geometry + kernel coefficients of one pass, in working precision T.
+template<typename T>
+struct EsParams
+{
+    int G;              // grid side
+    int support;        // W
+    int do_w;           // w-stacking (3-D) path
+    int plane;          // w-plane index processed (3-D), 0 in 2-D
+    int ntiles;         // tiles per axis = ceil(G / kTile)
+    int nbins;          // ntiles^2
+    T beta;             // full beta (table value * W)
+    T uv_scale;         // G * pixel_size
+    T w_scale;
+    T min_plane_w;
+};
+
+// Scratch owned by a plan (device pointers).
+struct BucketScratch
+{
+    uint32_t* table = nullptr;      // [num_chunks][nbins] counts / offsets
+    uint32_t* bin_count = nullptr;  // [nbins]
+    uint32_t* bin_start = nullptr;  // [nbins + 1]
+    uint32_t* item_start = nullptr; // [nbins + 1]
+    uint32_t* totals = nullptr;     // [2]: entries, items
+    uint32_t* totals_host = nullptr;// pinned host mirror of totals
+    void* recs = nullptr;           // bucketed records
+    size_t recs_bytes = 0;
+    size_t table_entries = 0;
+};
+
+// Number of visibility chunks used for a given visibility count.
+int num_chunks(int64_t num_vis);
+
+// Bucketing: returns host-visible totals (entries, items) after a stream
+// sync; fills scratch.recs (re-allocated if too small). Record layouts:
+//   grid, 2-D:  {pu, pv, vre*w, vim*w}
+//   grid, 3-D:  {pu, pv, vre*w, vim*w*flip, kw, 0, 0, 0}
+//   degrid:     {pu, pv, kw*flip (sign carries flip), index bits}
+template<typename T>
+int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
+        const T* uvw, const T* freq, const T* vis, const T* weight,
+        BucketScratch* s, hipStream_t stream, uint32_t* n_entries,
+        uint32_t* n_items);
+
+// Grid-mode tile accumulation: writes every cell of the G x G grid.
+template<typename T>
+int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
+        T* grid, hipStream_t stream);
+
+// Degrid-mode tile gather: vis[idx] += sum_taps grid * kernel.
+template<typename T>
+int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
+        const T* grid, T* vis, hipStream_t stream);
+
+// Image-plane kernels. image N x N (real), grid G x G complex (interleaved).
+// conv_corr: [N/2+1] normalised separable correction; quad_*: Gauss-Legendre
+// tables (kQuadratureBound entries); norm: C(0).
+template<typename T>
+struct ImageParams
+{
+    int N;
+    int G;
+    int support;
+    int do_w;
+    T pixel_size;
+    T norm;
+    T inv_w_scale;
+    T min_plane_w;
+    const T* conv_corr;
+    const T* quad_kernel;
+    const T* quad_nodes;
+    const T* quad_weights;
+};
+
+// 2-D grid path: dirty = (dirty + checker * Re(layer centre)) * corr.
+template<typename T>
+int screen_corr_2d(const ImageParams<T>& ip, const T* layer, T* dirty,
+        hipStream_t stream);
+
+// 3-D grid path, per plane: dirty += checker * Re(layer * phasor(w)).
+template<typename T>
+int screen_accumulate(const ImageParams<T>& ip, int plane, const T* layer,
+        T* dirty, hipStream_t stream);
+
+// dirty *= 1 / correction (2-D or 3-D correction), in place.
+template<typename T>
+int apply_correction(const ImageParams<T>& ip, T* dirty, hipStream_t stream);
+
+// Degrid path: grid (all G x G cells) = centre: checker * dirty * phasor(w)
+// (phasor = 1 in 2-D), zero elsewhere. If correct_in_place, the image is
+// first multiplied by 1/correction and written back (2-D fused form).
+template<typename T>
+int reverse_screen(const ImageParams<T>& ip, int plane, T* dirty,
+        bool correct_in_place, T* grid, hipStream_t stream);
+
+} // namespace sdp_es
+
+#endif

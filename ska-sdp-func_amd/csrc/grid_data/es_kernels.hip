@@ -1,0 +1,885 @@
+// HIP kernels of the MI355X-native ES-FFT (de)gridder. See es_kernels.h for
+// the data path. Per-visibility arithmetic (positions, tap ranges, the
+// exponential-of-semicircle taps, checkerboard sign, w<0 flip) follows the
+// reference kernels sdp_gridder_uvw_es_fft_kernels.cu:97-422 operation for
+// operation, in the same precision, so taps match the reference bit-for-bit
+// up to the libm exp/sqrt ulp; only the summation ORDER differs (LDS tile
+// accumulation instead of per-tap HBM atomics).
+#include <cmath>
+
+#include "es_kernels.h"
+#include "es_params.h"
+#include "../utility/sdp_hip.h"
+
+namespace sdp_es {
+namespace {
+
+constexpr double kSpeedOfLight = 299792458.0;
+constexpr double kPi = 3.1415926535897931;
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kScatterStride = kTile + 8;   // 72 = 8 (mod 32): conflict-free
+
+template<typename T> struct Vec2;
+template<> struct Vec2<float> { using type = float2; };
+template<> struct Vec2<double> { using type = double2; };
+
+// Exponential of semicircle, kernels.cu:97-102.
+template<typename T>
+__device__ __forceinline__ T es_tap(T beta, T x)
+{
+#pragma clang fp contract(off)
+    const T xx = x * x;
+    return (xx > T(1)) ? T(0) : exp(beta * (sqrt(T(1) - xx) - T(1)));
+}
+
+// Tap range of one visibility on the current w-plane (kernels.cu:150-196,
+// 301-347). Returns false if the visibility does not touch the plane.
+template<typename T>
+struct Footprint
+{
+    T pu, pv, kw, flip;
+    int u0, u1, v0, v1;
+};
+
+template<typename T>
+__device__ __forceinline__ bool footprint(const EsParams<T>& p, T u, T v,
+        T w, T freq, Footprint<T>& f)
+{
+#pragma clang fp contract(off)
+    f.flip = (p.do_w && w < T(0)) ? T(-1) : T(1);
+    const T inv_wavelength = f.flip * freq / T(kSpeedOfLight);
+    const T half_support = T(p.support) / T(2);
+    const int gmin = -p.G / 2, gmax = (p.G - 1) / 2;
+    f.pu = u * inv_wavelength * p.uv_scale;
+    f.pv = v * inv_wavelength * p.uv_scale;
+    f.u0 = max((int)ceil(f.pu - half_support), gmin);
+    f.u1 = min((int)floor(f.pu + half_support), gmax);
+    f.v0 = max((int)ceil(f.pv - half_support), gmin);
+    f.v1 = min((int)floor(f.pv + half_support), gmax);
+    f.kw = T(1);
+    if (p.do_w)
+    {
+        const T pos_w = (w * inv_wavelength - p.min_plane_w) * p.w_scale;
+        const int w0 = (int)ceil(pos_w - half_support);
+        const int w1 = (int)floor(pos_w + half_support);
+        if (p.plane < w0 || p.plane > w1) return false;
+        const T inv_half_support = T(1) / half_support;
+        f.kw = es_tap(p.beta, (T)(p.plane - pos_w) * inv_half_support);
+    }
+    return f.u0 <= f.u1 && f.v0 <= f.v1;
+}
+
+// Clamped tap range from a record position (same formula as footprint()).
+template<typename T>
+__device__ __forceinline__ void tap_range(const EsParams<T>& p, T pu, T pv,
+        int& u0, int& u1, int& v0, int& v1)
+{
+#pragma clang fp contract(off)
+    const T half_support = T(p.support) / T(2);
+    const int gmin = -p.G / 2, gmax = (p.G - 1) / 2;
+    u0 = max((int)ceil(pu - half_support), gmin);
+    u1 = min((int)floor(pu + half_support), gmax);
+    v0 = max((int)ceil(pv - half_support), gmin);
+    v1 = min((int)floor(pv + half_support), gmax);
+}
+
+template<typename T>
+__device__ __forceinline__ T tap_weight(const EsParams<T>& p, int u, int v,
+        T pu, T pv, T kw)
+{
+#pragma clang fp contract(off)
+    const T inv_half_support = T(1) / (T(p.support) / T(2));
+    const T ku = es_tap(p.beta, (T)(u - pu) * inv_half_support);
+    const T kv = es_tap(p.beta, (T)(v - pv) * inv_half_support);
+    T k = ku * kv * kw;
+    return ((u + v) & 1) ? -k : k;
+}
+
+// Records ------------------------------------------------------------------
+
+template<typename T, int MODE, bool DO_W>
+struct Rec
+{
+    static constexpr int kWords = (MODE == MODE_GRID && DO_W) ? 8 : 4;
+};
+
+__device__ __forceinline__ float idx_bits(float, uint64_t i)
+{
+    return __uint_as_float((uint32_t)i);
+}
+__device__ __forceinline__ double idx_bits(double, uint64_t i)
+{
+    return __longlong_as_double((long long)i);
+}
+__device__ __forceinline__ uint64_t bits_idx(float x)
+{
+    return (uint64_t)__float_as_uint(x);
+}
+__device__ __forceinline__ uint64_t bits_idx(double x)
+{
+    return (uint64_t)__double_as_longlong(x);
+}
+
+// Bucketing kernels ---------------------------------------------------------
+
+template<typename T, int MODE>
+__global__ __launch_bounds__(kThreads) void k_bucket_count(EsParams<T> p,
+        int64_t num_vis, int num_chan, int64_t chunk, const T* __restrict__ uvw,
+        const T* __restrict__ freq, uint32_t* __restrict__ table)
+{
+    __shared__ uint32_t hist[kBinsPerPass];
+    const int pass_base = blockIdx.y * kBinsPerPass;
+    const int nb = min(kBinsPerPass, p.nbins - pass_base);
+    for (int i = threadIdx.x; i < nb; i += kThreads) hist[i] = 0;
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * chunk;
+    const int64_t i1 = min(num_vis, i0 + chunk);
+    const int half = p.G / 2;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kThreads)
+    {
+        const int64_t r = i / num_chan;
+        const int c = (int)(i - r * num_chan);
+        Footprint<T> f;
+        if (!footprint(p, uvw[3 * r], uvw[3 * r + 1], uvw[3 * r + 2], freq[c],
+                f)) continue;
+        if (MODE == MODE_GRID)
+        {
+            const int tu0 = (f.u0 + half) / kTile, tu1 = (f.u1 + half) / kTile;
+            const int tv0 = (f.v0 + half) / kTile, tv1 = (f.v1 + half) / kTile;
+            for (int tu = tu0; tu <= tu1; ++tu)
+                for (int tv = tv0; tv <= tv1; ++tv)
+                {
+                    const int b = tu * p.ntiles + tv - pass_base;
+                    if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
+                }
+        }
+        else
+        {
+            const int b = ((f.u0 + half) / kTile) * p.ntiles +
+                    (f.v0 + half) / kTile - pass_base;
+            if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t* row = table + (size_t)blockIdx.x * p.nbins + pass_base;
+    for (int i = threadIdx.x; i < nb; i += kThreads) row[i] = hist[i];
+}
+
+// Per bin: exclusive prefix over chunks (in place) and the bin total.
+// Block = 16 waves; lane = bin, wave = contiguous range of chunks.
+__global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
+        int num_chunks, int nbins, uint32_t* __restrict__ bin_count)
+{
+    __shared__ uint32_t part[16][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int b = blockIdx.x * 64 + lane;
+    const int per = (num_chunks + 15) / 16;
+    const int c0 = wave * per, c1 = min(num_chunks, c0 + per);
+    uint32_t sum = 0;
+    if (b < nbins)
+        for (int c = c0; c < c1; ++c) sum += table[(size_t)c * nbins + b];
+    part[wave][lane] = sum;
+    __syncthreads();
+    if (wave == 0)
+    {
+        uint32_t run = 0;
+        for (int k = 0; k < 16; ++k)
+        {
+            const uint32_t t = part[k][lane];
+            part[k][lane] = run;
+            run += t;
+        }
+        if (b < nbins) bin_count[b] = run;
+    }
+    __syncthreads();
+    if (b < nbins)
+    {
+        uint32_t run = part[wave][lane];
+        for (int c = c0; c < c1; ++c)
+        {
+            const size_t k = (size_t)c * nbins + b;
+            const uint32_t t = table[k];
+            table[k] = run;
+            run += t;
+        }
+    }
+}
+
+// Exclusive prefix of bin totals and of work items (pieces of <= kPiece
+// entries, at least one per bin). One block of 1024 threads.
+__global__ __launch_bounds__(1024) void k_scan_bins(
+        const uint32_t* __restrict__ bin_count, int nbins,
+        uint32_t* __restrict__ bin_start, uint32_t* __restrict__ item_start,
+        uint32_t* __restrict__ totals)
+{
+    __shared__ uint32_t s_cnt[1024], s_itm[1024];
+    const int t = threadIdx.x;
+    const int per = (nbins + 1023) / 1024;
+    const int b0 = min(nbins, t * per), b1 = min(nbins, b0 + per);
+    uint32_t cnt = 0, itm = 0;
+    for (int b = b0; b < b1; ++b)
+    {
+        const uint32_t n = bin_count[b];
+        cnt += n;
+        itm += max(1u, (n + kPiece - 1) / kPiece);
+    }
+    s_cnt[t] = cnt;
+    s_itm[t] = itm;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1)   // inclusive Hillis-Steele
+    {
+        const uint32_t a = (t >= off) ? s_cnt[t - off] : 0;
+        const uint32_t c = (t >= off) ? s_itm[t - off] : 0;
+        __syncthreads();
+        s_cnt[t] += a;
+        s_itm[t] += c;
+        __syncthreads();
+    }
+    uint32_t run_c = s_cnt[t] - cnt, run_i = s_itm[t] - itm;
+    for (int b = b0; b < b1; ++b)
+    {
+        const uint32_t n = bin_count[b];
+        bin_start[b] = run_c;
+        item_start[b] = run_i;
+        run_c += n;
+        run_i += max(1u, (n + kPiece - 1) / kPiece);
+    }
+    if (t == 1023)
+    {
+        bin_start[nbins] = s_cnt[1023];
+        item_start[nbins] = s_itm[1023];
+        totals[0] = s_cnt[1023];
+        totals[1] = s_itm[1023];
+    }
+}
+
+template<typename T, int MODE, bool DO_W>
+__global__ __launch_bounds__(kThreads) void k_bucket_fill(EsParams<T> p,
+        int64_t num_vis, int num_chan, int64_t chunk, const T* __restrict__ uvw,
+        const T* __restrict__ freq, const T* __restrict__ vis,
+        const T* __restrict__ weight, const uint32_t* __restrict__ table,
+        const uint32_t* __restrict__ bin_start, T* __restrict__ recs)
+{
+    __shared__ uint32_t cursor[kBinsPerPass];
+    constexpr int kWords = Rec<T, MODE, DO_W>::kWords;
+    const int pass_base = blockIdx.y * kBinsPerPass;
+    const int nb = min(kBinsPerPass, p.nbins - pass_base);
+    const uint32_t* row = table + (size_t)blockIdx.x * p.nbins + pass_base;
+    for (int i = threadIdx.x; i < nb; i += kThreads)
+        cursor[i] = bin_start[pass_base + i] + row[i];
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * chunk;
+    const int64_t i1 = min(num_vis, i0 + chunk);
+    const int half = p.G / 2;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kThreads)
+    {
+        const int64_t r = i / num_chan;
+        const int c = (int)(i - r * num_chan);
+        Footprint<T> f;
+        if (!footprint(p, uvw[3 * r], uvw[3 * r + 1], uvw[3 * r + 2], freq[c],
+                f)) continue;
+        T rec[kWords];
+        rec[0] = f.pu;
+        rec[1] = f.pv;
+        if constexpr (MODE == MODE_GRID)
+        {
+            // kernels.cu:163-167: weight, then conjugate for w < 0.
+            const T wt = weight[i];
+            rec[2] = vis[2 * i] * wt;
+            T vim = vis[2 * i + 1] * wt;
+            vim *= f.flip;
+            rec[3] = vim;
+            if constexpr (DO_W && kWords == 8)
+            {
+                rec[4] = f.kw;
+                rec[5] = rec[6] = rec[7] = T(0);
+            }
+            const int tu0 = (f.u0 + half) / kTile, tu1 = (f.u1 + half) / kTile;
+            const int tv0 = (f.v0 + half) / kTile, tv1 = (f.v1 + half) / kTile;
+            for (int tu = tu0; tu <= tu1; ++tu)
+                for (int tv = tv0; tv <= tv1; ++tv)
+                {
+                    const int b = tu * p.ntiles + tv - pass_base;
+                    if (b < 0 || b >= nb) continue;
+                    const uint32_t pos = atomicAdd(&cursor[b], 1u);
+                    T* dst = recs + (size_t)pos * kWords;
+#pragma unroll
+                    for (int k = 0; k < kWords; ++k) dst[k] = rec[k];
+                }
+        }
+        else
+        {
+            rec[2] = copysign(f.kw, f.flip);
+            rec[3] = idx_bits(T(0), (uint64_t)i);
+            const int b = ((f.u0 + half) / kTile) * p.ntiles +
+                    (f.v0 + half) / kTile - pass_base;
+            if (b < 0 || b >= nb) continue;
+            const uint32_t pos = atomicAdd(&cursor[b], 1u);
+            T* dst = recs + (size_t)pos * kWords;
+#pragma unroll
+            for (int k = 0; k < kWords; ++k) dst[k] = rec[k];
+        }
+    }
+}
+
+// Work item -> (bin, piece). item_start is strictly increasing.
+__device__ __forceinline__ int find_bin(const uint32_t* item_start, int nbins,
+        uint32_t item)
+{
+    int lo = 0, hi = nbins;
+    while (hi - lo > 1)
+    {
+        const int mid = (lo + hi) >> 1;
+        if (item_start[mid] <= item) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// Zero the grid cells of tiles that several work items share.
+template<typename T>
+__global__ __launch_bounds__(kThreads) void k_zero_shared_tiles(int G,
+        int ntiles, const uint32_t* __restrict__ item_start, T* grid)
+{
+    const int b = blockIdx.x;
+    if (item_start[b + 1] - item_start[b] <= 1) return;
+    const int r0 = (b / ntiles) * kTile, c0 = (b % ntiles) * kTile;
+    const int nr = min(kTile, G - r0), nc = min(kTile, G - c0);
+    for (int k = threadIdx.x; k < nr * nc * 2; k += kThreads)
+    {
+        const int r = k / (2 * nc), c = k - r * 2 * nc;
+        grid[((size_t)(r0 + r) * G + c0) * 2 + c] = T(0);
+    }
+}
+
+// Grid mode: one workgroup per work item. Tile accumulated in LDS (planar
+// re / im, row stride 72), written to HBM once.
+template<typename T, bool DO_W>
+__global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
+        const T* __restrict__ recs, const uint32_t* __restrict__ bin_start,
+        const uint32_t* __restrict__ item_start, T* __restrict__ grid)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int S = kScatterStride;
+    constexpr int kWords = Rec<T, MODE_GRID, DO_W>::kWords;
+    T* s_re = (T*)smem;
+    T* s_im = s_re + kTile * S;
+    for (int k = threadIdx.x; k < kTile * S; k += kThreads)
+    {
+        s_re[k] = T(0);
+        s_im[k] = T(0);
+    }
+    const uint32_t item = blockIdx.x;
+    const int b = find_bin(item_start, p.nbins, item);
+    const uint32_t piece = item - item_start[b];
+    const uint32_t npieces = item_start[b + 1] - item_start[b];
+    const uint32_t e0 = bin_start[b] + piece * kPiece;
+    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
+    const int half = p.G / 2;
+    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    const int tu0 = r0 - half, tv0 = c0 - half;   // signed coords of tile
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int du = lane >> 3, dv = lane & 7;
+    for (uint32_t e = e0 + wave; e < e1; e += kWaves)
+    {
+        const T* rec = recs + (size_t)e * kWords;
+        const T pu = rec[0], pv = rec[1], vre = rec[2], vim = rec[3];
+        const T kw = DO_W ? rec[4] : T(1);
+        int u0, u1, v0, v1;
+        tap_range(p, pu, pv, u0, u1, v0, v1);
+        // Only the taps inside this tile.
+        u0 = max(u0, tu0);
+        u1 = min(u1, tu0 + kTile - 1);
+        v0 = max(v0, tv0);
+        v1 = min(v1, tv0 + kTile - 1);
+        for (int ub = u0; ub <= u1; ub += 8)
+        {
+            for (int vb = v0; vb <= v1; vb += 8)
+            {
+                const int u = ub + du, v = vb + dv;
+                if (u <= u1 && v <= v1)
+                {
+                    const T k = tap_weight(p, u, v, pu, pv, kw);
+                    const int a = (u - tu0) * S + (v - tv0);
+                    atomicAdd(&s_re[a], vre * k);
+                    atomicAdd(&s_im[a], vim * k);
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    const int nr = min(kTile, p.G - r0), nc = min(kTile, p.G - c0);
+    if (npieces == 1)
+    {
+        // Plain stores: 2 cells (float) / 1 cell (double) = 16 B per lane.
+        constexpr int kCells = sizeof(T) == 4 ? 2 : 1;
+        constexpr int kPerRow = kTile / kCells;
+        for (int k = threadIdx.x; k < kTile * kPerRow; k += kThreads)
+        {
+            const int r = k / kPerRow, c = (k - r * kPerRow) * kCells;
+            if (r >= nr || c >= nc) continue;
+            T* dst = grid + ((size_t)(r0 + r) * p.G + c0 + c) * 2;
+            if (kCells == 2)
+            {
+                float4 v;
+                v.x = (float)s_re[r * S + c];
+                v.y = (float)s_im[r * S + c];
+                v.z = (float)s_re[r * S + c + 1];
+                v.w = (float)s_im[r * S + c + 1];
+                *(float4*)dst = v;
+            }
+            else
+            {
+                double2 v;
+                v.x = (double)s_re[r * S + c];
+                v.y = (double)s_im[r * S + c];
+                *(double2*)dst = v;
+            }
+        }
+    }
+    else
+    {
+        // Shared tile: 256 contiguous bytes of f32 adds per wave-instruction.
+        for (int k = threadIdx.x; k < kTile * 2 * kTile; k += kThreads)
+        {
+            const int r = k / (2 * kTile), f = k - r * 2 * kTile;
+            const int c = f >> 1;
+            if (r >= nr || c >= nc) continue;
+            const T val = (f & 1) ? s_im[r * S + c] : s_re[r * S + c];
+            if (val != T(0))
+                unsafeAtomicAdd(grid + ((size_t)(r0 + r) * p.G + c0) * 2 + f,
+                        val);
+        }
+    }
+}
+
+// Degrid mode: one workgroup per work item; the tile plus its support halo
+// is staged in LDS once, then each wave gathers one visibility at a time
+// (lane = tap) and reduces across the wave.
+template<typename T, bool DO_W>
+__global__ __launch_bounds__(kThreads) void k_gather(EsParams<T> p,
+        const T* __restrict__ recs, const uint32_t* __restrict__ bin_start,
+        const uint32_t* __restrict__ item_start, const T* __restrict__ grid,
+        T* __restrict__ vis, int wrows, int ws)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    T* w_re = (T*)smem;
+    T* w_im = w_re + wrows * ws;
+    const uint32_t item = blockIdx.x;
+    const int b = find_bin(item_start, p.nbins, item);
+    const uint32_t piece = item - item_start[b];
+    const uint32_t e0 = bin_start[b] + piece * kPiece;
+    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
+    if (e0 >= e1) return;   // empty tile: nothing to gather
+    const int half = p.G / 2;
+    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    const int tu0 = r0 - half, tv0 = c0 - half;
+    using T2 = typename Vec2<T>::type;
+    const T2* g2 = (const T2*)grid;
+    for (int k = threadIdx.x; k < wrows * wrows; k += kThreads)
+    {
+        const int r = k / wrows, c = k - r * wrows;
+        T2 val;
+        val.x = T(0);
+        val.y = T(0);
+        if (r0 + r < p.G && c0 + c < p.G)
+            val = g2[(size_t)(r0 + r) * p.G + c0 + c];
+        w_re[r * ws + c] = val.x;
+        w_im[r * ws + c] = val.y;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int du = lane >> 3, dv = lane & 7;
+    for (uint32_t e = e0 + wave; e < e1; e += kWaves)
+    {
+        const T* rec = recs + (size_t)e * 4;
+        const T pu = rec[0], pv = rec[1], kwf = rec[2];
+        const T kw = fabs(kwf);
+        int u0, u1, v0, v1;
+        tap_range(p, pu, pv, u0, u1, v0, v1);
+        T acc_re = T(0), acc_im = T(0);
+        for (int ub = u0; ub <= u1; ub += 8)
+        {
+            for (int vb = v0; vb <= v1; vb += 8)
+            {
+                const int u = ub + du, v = vb + dv;
+                if (u <= u1 && v <= v1)
+                {
+                    const T k = tap_weight(p, u, v, pu, pv, kw);
+                    const int a = (u - tu0) * ws + (v - tv0);
+                    acc_re += w_re[a] * k;
+                    acc_im += w_im[a] * k;
+                }
+            }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1)
+        {
+            acc_re += __shfl_xor(acc_re, off);
+            acc_im += __shfl_xor(acc_im, off);
+        }
+        if (lane == 0)
+        {
+            const uint64_t i = bits_idx(rec[3]);
+            const T flip = signbit(kwf) ? T(-1) : T(1);
+            vis[2 * i] += acc_re;
+            vis[2 * i + 1] += acc_im * flip;   // kernels.cu:267-268
+        }
+    }
+}
+
+// Image-plane kernels ---------------------------------------------------------
+
+// conv_corr device function, kernels.cu:69-87 (cos argument in double as the
+// reference's double PI literal promotes it).
+template<typename T>
+__device__ T conv_corr_n(const ImageParams<T>& ip, T k)
+{
+    const T support = (T)ip.support;
+    const uint32_t np = (uint32_t)ceil(T(1.5) * support + T(2));
+    T c = T(0);
+    for (uint32_t i = 0; i < np; ++i)
+    {
+        c = (T)((double)c + (double)ip.quad_kernel[i] *
+                cos(kPi * (double)k * (double)support *
+                (double)ip.quad_nodes[i]) * (double)ip.quad_weights[i]);
+    }
+    return c * support;
+}
+
+// 1 / correction at pixel offsets (i = |x| column, j = |y| row),
+// kernels.cu:711-740.
+template<typename T>
+__device__ T inv_correction(const ImageParams<T>& ip, int i, int j)
+{
+#pragma clang fp contract(off)
+    const T l_conv = ip.conv_corr[i], m_conv = ip.conv_corr[j];
+    T corr;
+    if (ip.do_w)
+    {
+        const T l = ip.pixel_size * (T)i, m = ip.pixel_size * (T)j;
+        const T n = sqrt(T(1) - l * l - m * m) - T(1);
+        T n_conv = conv_corr_n(ip, n * ip.inv_w_scale);
+        n_conv *= (ip.norm * ip.norm);
+        corr = l_conv * m_conv * n_conv;
+    }
+    else
+    {
+        corr = l_conv * m_conv * ip.norm * ip.norm;
+    }
+    return T(1) / corr;
+}
+
+__device__ __forceinline__ void sin_cos(float x, float* s, float* c)
+{
+    sincosf(x, s, c);
+}
+__device__ __forceinline__ void sin_cos(double x, double* s, double* c)
+{
+    sincos(x, s, c);
+}
+
+// w-screen phasor, kernels.cu:110-123.
+template<typename T>
+__device__ void phasor(const ImageParams<T>& ip, int plane, int i, int j,
+        T sign, T& re, T& im)
+{
+#pragma clang fp contract(off)
+    const T l = ip.pixel_size * (T)i, m = ip.pixel_size * (T)j;
+    const T w = (T)plane * ip.inv_w_scale + ip.min_plane_w;
+    const T sos = l * l + m * m;
+    const T nm1 = (-sos) / (sqrt(T(1) - sos) + T(1));
+    const T x = T(2) * T(kPi) * w * nm1;
+    const T xn = T(1) / (nm1 + T(1));
+    sin_cos(sign * x, &im, &re);
+    re *= xn;
+    im *= xn;
+}
+
+template<typename T>
+__global__ void k_screen_corr_2d(ImageParams<T> ip, const T* __restrict__ layer,
+        T* __restrict__ dirty)
+{
+#pragma clang fp contract(off)
+    const int h = ip.N / 2;
+    const int ix = blockIdx.x * blockDim.x + threadIdx.x;
+    const int iy = blockIdx.y * blockDim.y + threadIdx.y;
+    if (ix >= 2 * h || iy >= 2 * h) return;
+    const int x = ix - h, y = iy - h, gc = ip.G / 2;
+    T val = layer[((size_t)(gc + y) * ip.G + (gc + x)) * 2];
+    if ((ix + iy) & 1) val = -val;
+    T* d = dirty + (size_t)iy * ip.N + ix;
+    T out = *d + val;
+    out *= inv_correction(ip, abs(x), abs(y));
+    *d = out;
+}
+
+template<typename T>
+__global__ void k_screen_accumulate(ImageParams<T> ip, int plane,
+        const T* __restrict__ layer, T* __restrict__ dirty)
+{
+#pragma clang fp contract(off)
+    const int h = ip.N / 2;
+    const int ix = blockIdx.x * blockDim.x + threadIdx.x;
+    const int iy = blockIdx.y * blockDim.y + threadIdx.y;
+    if (ix >= 2 * h || iy >= 2 * h) return;
+    const int x = ix - h, y = iy - h, gc = ip.G / 2;
+    const size_t g = ((size_t)(gc + y) * ip.G + (gc + x)) * 2;
+    T re, im;
+    phasor(ip, plane, abs(x), abs(y), T(-1), re, im);
+    T val = layer[g] * re - layer[g + 1] * im;
+    if ((ix + iy) & 1) val = -val;
+    dirty[(size_t)iy * ip.N + ix] += val;
+}
+
+template<typename T>
+__global__ void k_apply_correction(ImageParams<T> ip, T* __restrict__ dirty)
+{
+    const int h = ip.N / 2;
+    const int ix = blockIdx.x * blockDim.x + threadIdx.x;
+    const int iy = blockIdx.y * blockDim.y + threadIdx.y;
+    if (ix >= 2 * h || iy >= 2 * h) return;
+    dirty[(size_t)iy * ip.N + ix] *= inv_correction(ip, abs(ix - h),
+            abs(iy - h));
+}
+
+// Whole-grid writer for degridding: centre = checker * dirty * phasor.
+template<typename T>
+__global__ void k_reverse_screen(ImageParams<T> ip, int plane,
+        T* __restrict__ dirty, int correct_in_place, T* __restrict__ grid)
+{
+#pragma clang fp contract(off)
+    const int gx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int gy = blockIdx.y * blockDim.y + threadIdx.y;
+    if (gx >= ip.G || gy >= ip.G) return;
+    const int h = ip.N / 2, gc = ip.G / 2;
+    const int x = gx - gc, y = gy - gc;
+    T re = T(0), im = T(0);
+    if (x >= -h && x < h && y >= -h && y < h)
+    {
+        T* d = dirty + (size_t)(y + h) * ip.N + (x + h);
+        T val = *d;
+        if (correct_in_place)
+        {
+            val *= inv_correction(ip, abs(x), abs(y));
+            *d = val;
+        }
+        if ((x + y) & 1) val = -val;
+        T pr = T(1), pi = T(0);
+        if (ip.do_w) phasor(ip, plane, abs(x), abs(y), T(1), pr, pi);
+        re = pr * val;
+        im = pi * val;
+    }
+    T* g = grid + ((size_t)gy * ip.G + gx) * 2;
+    g[0] = re;
+    g[1] = im;
+}
+
+dim3 image_blocks(int n)
+{
+    return dim3((unsigned)((n + 63) / 64), (unsigned)((n + 3) / 4));
+}
+
+} // namespace
+
+int num_chunks(int64_t num_vis)
+{
+    const int64_t by_size = (num_vis + 8191) / 8192;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxChunks, by_size));
+}
+
+template<typename T>
+int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
+        const T* uvw, const T* freq, const T* vis, const T* weight,
+        BucketScratch* s, hipStream_t stream, uint32_t* n_entries,
+        uint32_t* n_items)
+{
+    sdp_Error st = SDP_SUCCESS;
+    sdp_Error* status = &st;
+    const int64_t num_vis = num_rows * num_chan;
+    const int nc = num_chunks(num_vis);
+    const int64_t chunk = (num_vis + nc - 1) / nc;
+    const int passes = (p.nbins + kBinsPerPass - 1) / kBinsPerPass;
+    const dim3 grid_b(nc, passes);
+    if (mode == MODE_GRID)
+        k_bucket_count<T, MODE_GRID><<<grid_b, kThreads, 0, stream>>>(
+                p, num_vis, num_chan, chunk, uvw, freq, s->table);
+    else
+        k_bucket_count<T, MODE_DEGRID><<<grid_b, kThreads, 0, stream>>>(
+                p, num_vis, num_chan, chunk, uvw, freq, s->table);
+    SDP_HIP_CHECK_LAUNCH(status);
+    k_scan_columns<<<(p.nbins + 63) / 64, 1024, 0, stream>>>(
+            s->table, nc, p.nbins, s->bin_count);
+    SDP_HIP_CHECK_LAUNCH(status);
+    k_scan_bins<<<1, 1024, 0, stream>>>(s->bin_count, p.nbins, s->bin_start,
+            s->item_start, s->totals);
+    SDP_HIP_CHECK_LAUNCH(status);
+    SDP_HIP_CHECK(hipMemcpyAsync(s->totals_host, s->totals,
+            2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream), status);
+    SDP_HIP_CHECK(hipStreamSynchronize(stream), status);
+    if (*status) return *status;
+    *n_entries = s->totals_host[0];
+    *n_items = s->totals_host[1];
+    const int words = (mode == MODE_GRID && p.do_w) ? 8 : 4;
+    const size_t need = (size_t)(*n_entries) * words * sizeof(T);
+    if (need > s->recs_bytes)
+    {
+        if (s->recs) SDP_HIP_CHECK(hipFree(s->recs), status);
+        const size_t bytes = need + need / 8 + 4096;
+        s->recs = nullptr;
+        SDP_HIP_CHECK(hipMalloc(&s->recs, bytes), status);
+        if (*status) return SDP_ERR_MEM_ALLOC_FAILURE;
+        s->recs_bytes = bytes;
+    }
+    T* recs = (T*)s->recs;
+    if (mode == MODE_GRID)
+    {
+        if (p.do_w)
+            k_bucket_fill<T, MODE_GRID, true><<<grid_b, kThreads, 0, stream>>>(
+                    p, num_vis, num_chan, chunk, uvw, freq, vis, weight,
+                    s->table, s->bin_start, recs);
+        else
+            k_bucket_fill<T, MODE_GRID, false><<<grid_b, kThreads, 0,
+                    stream>>>(p, num_vis, num_chan, chunk, uvw, freq, vis,
+                    weight, s->table, s->bin_start, recs);
+    }
+    else
+    {
+        k_bucket_fill<T, MODE_DEGRID, false><<<grid_b, kThreads, 0, stream>>>(
+                p, num_vis, num_chan, chunk, uvw, freq, vis, weight,
+                s->table, s->bin_start, recs);
+    }
+    SDP_HIP_CHECK_LAUNCH(status);
+    return *status;
+}
+
+template<typename T>
+int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
+        T* grid, hipStream_t stream)
+{
+    sdp_Error st = SDP_SUCCESS;
+    sdp_Error* status = &st;
+    k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
+            p.G, p.ntiles, s.item_start, grid);
+    SDP_HIP_CHECK_LAUNCH(status);
+    const size_t lds = 2 * (size_t)kTile * kScatterStride * sizeof(T);
+    if (p.do_w)
+    {
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter<T, true>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), status);
+        k_scatter<T, true><<<n_items, kThreads, lds, stream>>>(
+                p, (const T*)s.recs, s.bin_start, s.item_start, grid);
+    }
+    else
+    {
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter<T, false>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), status);
+        k_scatter<T, false><<<n_items, kThreads, lds, stream>>>(
+                p, (const T*)s.recs, s.bin_start, s.item_start, grid);
+    }
+    SDP_HIP_CHECK_LAUNCH(status);
+    return *status;
+}
+
+template<typename T>
+int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
+        const T* grid, T* vis, hipStream_t stream)
+{
+    sdp_Error st = SDP_SUCCESS;
+    sdp_Error* status = &st;
+    const int wrows = kTile + p.support;
+    int ws = wrows;
+    while (ws % 32 != 8 && ws % 32 != 24) ++ws;
+    const size_t lds = 2 * (size_t)wrows * ws * sizeof(T);
+    if (lds > 160 * 1024)
+    {
+        SDP_LOG_ERROR("Support %d too large for the LDS window", p.support);
+        return SDP_ERR_INVALID_ARGUMENT;
+    }
+    if (p.do_w)
+    {
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_gather<T, true>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), status);
+        k_gather<T, true><<<n_items, kThreads, lds, stream>>>(p,
+                (const T*)s.recs, s.bin_start, s.item_start, grid, vis, wrows,
+                ws);
+    }
+    else
+    {
+        SDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_gather<T, false>,
+                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), status);
+        k_gather<T, false><<<n_items, kThreads, lds, stream>>>(p,
+                (const T*)s.recs, s.bin_start, s.item_start, grid, vis, wrows,
+                ws);
+    }
+    SDP_HIP_CHECK_LAUNCH(status);
+    return *status;
+}
+
+template<typename T>
+int screen_corr_2d(const ImageParams<T>& ip, const T* layer, T* dirty,
+        hipStream_t stream)
+{
+    sdp_Error st = SDP_SUCCESS;
+    k_screen_corr_2d<T><<<image_blocks(ip.N), dim3(64, 4), 0, stream>>>(
+            ip, layer, dirty);
+    SDP_HIP_CHECK_LAUNCH(&st);
+    return st;
+}
+
+template<typename T>
+int screen_accumulate(const ImageParams<T>& ip, int plane, const T* layer,
+        T* dirty, hipStream_t stream)
+{
+    sdp_Error st = SDP_SUCCESS;
+    k_screen_accumulate<T><<<image_blocks(ip.N), dim3(64, 4), 0, stream>>>(
+            ip, plane, layer, dirty);
+    SDP_HIP_CHECK_LAUNCH(&st);
+    return st;
+}
+
+template<typename T>
+int apply_correction(const ImageParams<T>& ip, T* dirty, hipStream_t stream)
+{
+    sdp_Error st = SDP_SUCCESS;
+    k_apply_correction<T><<<image_blocks(ip.N), dim3(64, 4), 0, stream>>>(
+            ip, dirty);
+    SDP_HIP_CHECK_LAUNCH(&st);
+    return st;
+}
+
+template<typename T>
+int reverse_screen(const ImageParams<T>& ip, int plane, T* dirty,
+        bool correct_in_place, T* grid, hipStream_t stream)
+{
+    sdp_Error st = SDP_SUCCESS;
+    k_reverse_screen<T><<<image_blocks(ip.G), dim3(64, 4), 0, stream>>>(
+            ip, plane, dirty, correct_in_place ? 1 : 0, grid);
+    SDP_HIP_CHECK_LAUNCH(&st);
+    return st;
+}
+
+#define SDP_ES_INSTANTIATE(T) \
+    template int bucket<T>(const EsParams<T>&, Mode, int64_t, int, const T*, \
+            const T*, const T*, const T*, BucketScratch*, hipStream_t, \
+            uint32_t*, uint32_t*); \
+    template int scatter<T>(const EsParams<T>&, const BucketScratch&, \
+            uint32_t, T*, hipStream_t); \
+    template int gather<T>(const EsParams<T>&, const BucketScratch&, \
+            uint32_t, const T*, T*, hipStream_t); \
+    template int screen_corr_2d<T>(const ImageParams<T>&, const T*, T*, \
+            hipStream_t); \
+    template int screen_accumulate<T>(const ImageParams<T>&, int, const T*, \
+            T*, hipStream_t); \
+    template int apply_correction<T>(const ImageParams<T>&, T*, hipStream_t); \
+    template int reverse_screen<T>(const ImageParams<T>&, int, T*, bool, T*, \
+            hipStream_t);
+
+SDP_ES_INSTANTIATE(float)
+SDP_ES_INSTANTIATE(double)
+
+} // namespace sdp_es

@@ -1,0 +1,727 @@
+// MI355X-native ES-FFT (de)gridder: plan, argument checks and driver.
+//
+// Replaces src/ska-sdp-func/grid_data/sdp_gridder_uvw_es_fft.cpp of the
+// reference. Argument checks and their error codes/messages follow
+// sdp_gridder_check_buffers (:72-243) and check_parameters (:246-262); the
+// plan geometry (w-planes, scales, correction tables) follows create_plan
+// (:305-424). The compute path is different: per w-plane, visibilities are
+// bucketed by grid tile and scattered through LDS (es_kernels.hip), the FFT
+// is rocFFT with a plan cached in the gridder plan, and the image-plane
+// steps are fused (2-D: one kernel for screen + correction).
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "ska-sdp-func/grid_data/sdp_gridder_uvw_es_fft.h"
+#include "es_kernels.h"
+#include "es_params.h"
+#include "../fft/fft2d.h"
+#include "../utility/sdp_hip.h"
+
+struct sdp_GridderUvwEsFft
+{
+    double pixsize_x_rad;
+    double pixsize_y_rad;
+    double epsilon;
+    int do_wstacking;
+    int num_rows;
+    int num_chan;
+    int image_size;
+    int grid_size;
+    int support;
+    double beta;          // full beta (table beta * support)
+    double pixel_size;
+    double uv_scale;
+    double min_plane_w;
+    double max_plane_w;
+    double min_abs_w;
+    double max_abs_w;
+    int num_total_w_grids;
+    double w_scale;
+    double inv_w_scale;
+    double inv_w_range;
+    double conv_corr_norm_factor;
+    int is_double;
+
+    // Device state.
+    void* grid;                 // G x G complex plane
+    void* tables;               // conv_corr | quad kernel | nodes | weights
+    int ntiles;
+    int nbins;
+    sdp_es::BucketScratch scratch;
+    sdp_fft::Plan2D* fft;
+    hipStream_t stream;
+
+    // Timing.
+    int timing;
+    hipEvent_t ev[5];
+    double acc_ms[5];
+    int have_timing;
+};
+
+namespace {
+
+const char* kMsgLocation = "Memory location mismatch.";
+
+void check_buffers(const sdp_Mem* uvw, const sdp_Mem* freq_hz,
+        const sdp_Mem* vis, const sdp_Mem* weight, const sdp_Mem* dirty_image,
+        bool do_degridding, sdp_Error* status)
+{
+    if (*status) return;
+    // dirty_image may be NULL (split-gridding API): its checks are skipped.
+    if (!dirty_image) dirty_image = weight;
+    const bool have_image = dirty_image != weight;
+    const sdp_MemLocation loc = sdp_mem_location(uvw);
+    if (loc != sdp_mem_location(freq_hz) || loc != sdp_mem_location(vis) ||
+            loc != sdp_mem_location(weight) ||
+            loc != sdp_mem_location(dirty_image))
+    {
+        *status = SDP_ERR_MEM_LOCATION;
+        SDP_LOG_ERROR("%s", kMsgLocation);
+        return;
+    }
+    struct { const sdp_Mem* m; bool complex; const char* msg; } kinds[] = {
+        {uvw, false, "uvw values must be real."},
+        {freq_hz, false, "Frequency values must be real."},
+        {vis, true, "Visibility values must be complex."},
+        {weight, false, "Weight values must be real."},
+        {dirty_image, false, "Dirty image must be real"},
+    };
+    for (const auto& k : kinds)
+    {
+        if ((sdp_mem_is_complex(k.m) != 0) != k.complex)
+        {
+            *status = SDP_ERR_DATA_TYPE;
+            SDP_LOG_ERROR("%s", k.msg);
+            return;
+        }
+    }
+    const int64_t num_vis = sdp_mem_shape_dim(vis, 0);
+    const int64_t num_chan = sdp_mem_shape_dim(vis, 1);
+    if (sdp_mem_shape_dim(uvw, 0) != num_vis)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("The number of rows in uvw and vis must match.");
+        return;
+    }
+    if (sdp_mem_shape_dim(uvw, 1) != 3)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("uvw must be N x 3.");
+        return;
+    }
+    if (sdp_mem_shape_dim(freq_hz, 0) != num_chan)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("The number of channels in vis and freq_hz must match.");
+        return;
+    }
+    if (sdp_mem_shape_dim(weight, 0) != num_vis ||
+            sdp_mem_shape_dim(weight, 1) != num_chan)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("weight and vis must be the same size.");
+        return;
+    }
+    if (have_image &&
+            sdp_mem_shape_dim(dirty_image, 0) != sdp_mem_shape_dim(dirty_image, 1))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Dirty image must be square.");
+        return;
+    }
+    const bool dbl = sdp_mem_type(uvw) == SDP_MEM_DOUBLE;
+    const sdp_MemType want_real = dbl ? SDP_MEM_DOUBLE : SDP_MEM_FLOAT;
+    const sdp_MemType want_cplx =
+            dbl ? SDP_MEM_COMPLEX_DOUBLE : SDP_MEM_COMPLEX_FLOAT;
+    if (sdp_mem_type(freq_hz) != want_real || sdp_mem_type(vis) != want_cplx ||
+            sdp_mem_type(weight) != want_real ||
+            sdp_mem_type(dirty_image) != want_real)
+    {
+        *status = SDP_ERR_DATA_TYPE;
+        SDP_LOG_ERROR("All buffers must be the same precision.");
+        return;
+    }
+    if (!sdp_mem_is_c_contiguous(uvw) || !sdp_mem_is_c_contiguous(freq_hz) ||
+            !sdp_mem_is_c_contiguous(vis) || !sdp_mem_is_c_contiguous(weight) ||
+            !sdp_mem_is_c_contiguous(dirty_image))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("All input arrays must be C contiguous");
+        return;
+    }
+    if (do_degridding && sdp_mem_is_read_only(vis))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Visibility data must be writable.");
+        return;
+    }
+    if (have_image && !do_degridding && sdp_mem_is_read_only(dirty_image))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Dirty image must be writable.");
+        return;
+    }
+}
+
+void check_parameters(double px, double py, sdp_Error* status)
+{
+    if (*status) return;
+    if (px != py)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Only square images supported, so pixsize_x_rad and "
+                "pixsize_y_rad must be equal.");
+        SDP_LOG_ERROR("pixsize_x_rad is %.12e", px);
+        SDP_LOG_ERROR("pixsize_y_rad is %.12e", py);
+    }
+}
+
+size_t real_size(const sdp_GridderUvwEsFft* plan)
+{
+    return plan->is_double ? sizeof(double) : sizeof(float);
+}
+
+// (Re)allocate the bucketing count table for num_vis visibilities.
+void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
+        sdp_Error* status)
+{
+    if (*status) return;
+    sdp_es::BucketScratch& s = plan->scratch;
+    const size_t need = (size_t)sdp_es::num_chunks(num_vis) * plan->nbins;
+    if (need > s.table_entries)
+    {
+        if (s.table) SDP_HIP_CHECK(hipFree(s.table), status);
+        s.table = nullptr;
+        SDP_HIP_CHECK(hipMalloc(&s.table, need * sizeof(uint32_t)), status);
+        s.table_entries = *status ? 0 : need;
+    }
+}
+
+void timing_mark(sdp_GridderUvwEsFft* plan, int k)
+{
+    if (plan->timing) (void)hipEventRecord(plan->ev[k], plan->stream);
+}
+
+// Sum phase times of one plane into acc_ms (syncs the last event).
+void timing_collect(sdp_GridderUvwEsFft* plan)
+{
+    if (!plan->timing) return;
+    (void)hipEventSynchronize(plan->ev[4]);
+    for (int k = 0; k < 4; ++k)
+    {
+        float ms = 0.0f;
+        (void)hipEventElapsedTime(&ms, plan->ev[k], plan->ev[k + 1]);
+        plan->acc_ms[k] += ms;
+    }
+}
+
+template<typename T>
+sdp_es::EsParams<T> es_params(const sdp_GridderUvwEsFft* plan, int plane)
+{
+    sdp_es::EsParams<T> p;
+    p.G = plan->grid_size;
+    p.support = plan->support;
+    p.do_w = plan->do_wstacking;
+    p.plane = plane;
+    p.ntiles = plan->ntiles;
+    p.nbins = plan->nbins;
+    p.beta = (T)plan->beta;
+    p.uv_scale = (T)plan->uv_scale;
+    p.w_scale = (T)plan->w_scale;
+    p.min_plane_w = (T)plan->min_plane_w;
+    return p;
+}
+
+template<typename T>
+sdp_es::ImageParams<T> image_params(const sdp_GridderUvwEsFft* plan)
+{
+    sdp_es::ImageParams<T> ip;
+    ip.N = plan->image_size;
+    ip.G = plan->grid_size;
+    ip.support = plan->support;
+    ip.do_w = plan->do_wstacking;
+    ip.pixel_size = (T)plan->pixel_size;
+    ip.norm = (T)plan->conv_corr_norm_factor;
+    ip.inv_w_scale = (T)plan->inv_w_scale;
+    ip.min_plane_w = (T)plan->min_plane_w;
+    const T* t = (const T*)plan->tables;
+    ip.conv_corr = t;
+    ip.quad_kernel = t + plan->image_size / 2 + 1;
+    ip.quad_nodes = ip.quad_kernel + sdp_es::kQuadratureBound;
+    ip.quad_weights = ip.quad_nodes + sdp_es::kQuadratureBound;
+    return ip;
+}
+
+// Bucket + scatter one plane of this call's visibilities into grid.
+template<typename T>
+void scatter_plane(sdp_GridderUvwEsFft* plan, int plane, int64_t rows,
+        int chan, const T* uvw, const T* freq, const T* vis, const T* weight,
+        T* grid, sdp_Error* status)
+{
+    if (*status) return;
+    const sdp_es::EsParams<T> p = es_params<T>(plan, plane);
+    uint32_t n_entries = 0, n_items = 0;
+    timing_mark(plan, 0);
+    int e = sdp_es::bucket<T>(p, sdp_es::MODE_GRID, rows, chan, uvw, freq,
+            vis, weight, &plan->scratch, plan->stream, &n_entries, &n_items);
+    if (e) { *status = (sdp_Error)e; return; }
+    timing_mark(plan, 1);
+    e = sdp_es::scatter<T>(p, plan->scratch, n_items, grid, plan->stream);
+    if (e) { *status = (sdp_Error)e; return; }
+    timing_mark(plan, 2);
+}
+
+template<typename T>
+void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
+        const T* uvw, const T* freq, const T* vis, const T* weight, T* dirty,
+        sdp_Error* status)
+{
+    ensure_scratch(plan, rows * chan, status);
+    const sdp_es::ImageParams<T> ip = image_params<T>(plan);
+    T* grid = (T*)plan->grid;
+    for (int plane = 0; plane < plan->num_total_w_grids && !*status; ++plane)
+    {
+        scatter_plane<T>(plan, plane, rows, chan, uvw, freq, vis, weight,
+                grid, status);
+        sdp_fft::exec_2d(plan->fft, grid, false, plan->stream, status);
+        timing_mark(plan, 3);
+        if (*status) return;
+        int e = plan->do_wstacking ?
+                sdp_es::screen_accumulate<T>(ip, plane, grid, dirty,
+                        plan->stream) :
+                sdp_es::screen_corr_2d<T>(ip, grid, dirty, plan->stream);
+        if (plan->do_wstacking &&
+                plane == plan->num_total_w_grids - 1 && !e)
+        {
+            e = sdp_es::apply_correction<T>(ip, dirty, plan->stream);
+        }
+        if (e) { *status = (sdp_Error)e; return; }
+        timing_mark(plan, 4);
+        timing_collect(plan);
+    }
+}
+
+template<typename T>
+void run_degrid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
+        const T* uvw, const T* freq, T* vis, T* dirty, sdp_Error* status)
+{
+    ensure_scratch(plan, rows * chan, status);
+    if (*status) return;
+    const sdp_es::ImageParams<T> ip = image_params<T>(plan);
+    T* grid = (T*)plan->grid;
+    int e = 0;
+    if (plan->do_wstacking)
+    {
+        e = sdp_es::apply_correction<T>(ip, dirty, plan->stream);
+        if (e) { *status = (sdp_Error)e; return; }
+    }
+    for (int plane = 0; plane < plan->num_total_w_grids && !*status; ++plane)
+    {
+        const sdp_es::EsParams<T> p = es_params<T>(plan, plane);
+        timing_mark(plan, 0);
+        uint32_t n_entries = 0, n_items = 0;
+        e = sdp_es::bucket<T>(p, sdp_es::MODE_DEGRID, rows, chan, uvw, freq,
+                nullptr, nullptr, &plan->scratch, plan->stream, &n_entries,
+                &n_items);
+        if (e) { *status = (sdp_Error)e; return; }
+        timing_mark(plan, 1);
+        e = sdp_es::reverse_screen<T>(ip, plane, dirty,
+                !plan->do_wstacking, grid, plan->stream);
+        if (e) { *status = (sdp_Error)e; return; }
+        timing_mark(plan, 2);
+        sdp_fft::exec_2d(plan->fft, grid, true, plan->stream, status);
+        if (*status) return;
+        timing_mark(plan, 3);
+        e = sdp_es::gather<T>(p, plan->scratch, n_items, grid, vis,
+                plan->stream);
+        if (e) { *status = (sdp_Error)e; return; }
+        timing_mark(plan, 4);
+        timing_collect(plan);
+    }
+}
+
+void timing_begin(sdp_GridderUvwEsFft* plan)
+{
+    for (int k = 0; k < 5; ++k) plan->acc_ms[k] = 0.0;
+    plan->have_timing = 0;
+}
+
+void timing_end(sdp_GridderUvwEsFft* plan, double wall_ms)
+{
+    if (!plan->timing) return;
+    plan->acc_ms[4] = wall_ms;
+    plan->have_timing = 1;
+}
+
+} // namespace
+
+extern "C" {
+
+void sdp_gridder_uvw_es_fft_free_plan(sdp_GridderUvwEsFft* plan)
+{
+    if (!plan) return;
+    if (plan->grid) (void)hipFree(plan->grid);
+    if (plan->tables) (void)hipFree(plan->tables);
+    sdp_es::BucketScratch& s = plan->scratch;
+    if (s.table) (void)hipFree(s.table);
+    if (s.bin_count) (void)hipFree(s.bin_count);
+    if (s.recs) (void)hipFree(s.recs);
+    if (s.totals_host) (void)hipHostFree(s.totals_host);
+    sdp_fft::destroy_2d(plan->fft);
+    if (plan->timing)
+        for (int k = 0; k < 5; ++k) (void)hipEventDestroy(plan->ev[k]);
+    free(plan);
+}
+
+sdp_GridderUvwEsFft* sdp_gridder_uvw_es_fft_create_plan(
+        const sdp_Mem* uvw, const sdp_Mem* freq_hz, const sdp_Mem* vis,
+        const sdp_Mem* weight, const sdp_Mem* dirty_image,
+        const double pixel_size_x_rad, const double pixel_size_y_rad,
+        const double epsilon, const double min_abs_w, const double max_abs_w,
+        const int do_w_stacking, sdp_Error* status)
+{
+    if (*status) return nullptr;
+    check_parameters(pixel_size_x_rad, pixel_size_y_rad, status);
+    check_buffers(uvw, freq_hz, vis, weight, dirty_image, false, status);
+    if (*status) return nullptr;
+
+    sdp_GridderUvwEsFft* plan =
+            (sdp_GridderUvwEsFft*)calloc(1, sizeof(sdp_GridderUvwEsFft));
+    plan->pixsize_x_rad = pixel_size_x_rad;
+    plan->pixsize_y_rad = pixel_size_y_rad;
+    plan->pixel_size = pixel_size_x_rad;
+    plan->epsilon = epsilon;
+    plan->do_wstacking = do_w_stacking ? 1 : 0;
+    plan->num_rows = (int)sdp_mem_shape_dim(vis, 0);
+    plan->num_chan = (int)sdp_mem_shape_dim(vis, 1);
+    plan->image_size = (int)sdp_mem_shape_dim(dirty_image, 0);
+    plan->is_double = (sdp_mem_type(vis) & SDP_MEM_DOUBLE) ? 1 : 0;
+
+    double beta_w = 0.0;
+    sdp_es::params_from_epsilon(epsilon, plan->image_size,
+            plan->is_double != 0, &plan->grid_size, &plan->support, &beta_w);
+    plan->beta = beta_w * plan->support;
+    plan->uv_scale = plan->grid_size * plan->pixel_size;
+
+    // w-plane geometry, sdp_gridder_uvw_es_fft.cpp:346-383.
+    if (plan->do_wstacking)
+    {
+        const double x0 = -0.5 * plan->image_size * plan->pixel_size;
+        const double y0 = x0;
+        double nmin = sqrt(std::max(1.0 - x0 * x0 - y0 * y0, 0.0)) - 1.0;
+        if (x0 * x0 + y0 * y0 > 1.0)
+        {
+            nmin = -sqrt(fabs(1.0 - x0 * x0 - y0 * y0)) - 1.0;
+        }
+        double w_scale = 0.25 / fabs(nmin);
+        int nw = (int)((max_abs_w - min_abs_w) / w_scale + 2);
+        w_scale = 1.0 / ((1.0 + 1e-13) * (max_abs_w - min_abs_w) / (nw - 1));
+        plan->min_plane_w = min_abs_w - (0.5 * plan->support - 1.0) / w_scale;
+        plan->max_plane_w = max_abs_w + (0.5 * plan->support - 1.0) / w_scale;
+        plan->num_total_w_grids = nw + plan->support - 2;
+        plan->min_abs_w = min_abs_w;
+        plan->max_abs_w = max_abs_w;
+        plan->w_scale = w_scale;
+        plan->inv_w_range = plan->max_plane_w - plan->min_plane_w;
+    }
+    else
+    {
+        plan->num_total_w_grids = 1;
+        plan->inv_w_range = 1.0;
+        plan->w_scale = 1.0;
+    }
+    plan->inv_w_scale = 1.0 / plan->w_scale;
+
+    // Correction tables (host, double), then cast to working precision.
+    const int nc = plan->image_size / 2 + 1;
+    const int q = sdp_es::kQuadratureBound;
+    double* host = (double*)calloc(nc + 3 * q, sizeof(double));
+    plan->conv_corr_norm_factor = sdp_es::gauss_legendre_conv_kernel(
+            plan->image_size, plan->grid_size, plan->support, plan->beta,
+            host + nc, host + nc + q, host + nc + 2 * q, host);
+    plan->ntiles = (plan->grid_size + sdp_es::kTile - 1) / sdp_es::kTile;
+    plan->nbins = plan->ntiles * plan->ntiles;
+    plan->stream = 0;
+
+    if (!sdp_hip::device_available())
+    {
+        // Same outcome as the reference built without GPU support.
+        *status = SDP_ERR_MEM_LOCATION;
+        SDP_LOG_ERROR("Cannot allocate GPU memory: no HIP device available.");
+        free(host);
+        sdp_gridder_uvw_es_fft_free_plan(plan);
+        return nullptr;
+    }
+    const size_t rs = real_size(plan);
+    const size_t ntab = nc + 3 * q;
+    SDP_HIP_CHECK(hipMalloc(&plan->tables, ntab * rs), status);
+    if (!*status)
+    {
+        if (plan->is_double)
+        {
+            SDP_HIP_CHECK(hipMemcpy(plan->tables, host, ntab * rs,
+                    hipMemcpyHostToDevice), status);
+        }
+        else
+        {
+            float* f = (float*)malloc(ntab * sizeof(float));
+            for (size_t i = 0; i < ntab; ++i) f[i] = (float)host[i];
+            SDP_HIP_CHECK(hipMemcpy(plan->tables, f, ntab * rs,
+                    hipMemcpyHostToDevice), status);
+            free(f);
+        }
+    }
+    free(host);
+    const size_t cells = (size_t)plan->grid_size * plan->grid_size;
+    SDP_HIP_CHECK(hipMalloc(&plan->grid, cells * 2 * rs), status);
+    sdp_es::BucketScratch& s = plan->scratch;
+    const size_t nb = (size_t)plan->nbins;
+    if (!*status)
+    {
+        // bin_count | bin_start | item_start | totals in one allocation.
+        SDP_HIP_CHECK(hipMalloc(&s.bin_count,
+                (nb + 2 * (nb + 1) + 2) * sizeof(uint32_t)), status);
+        if (!*status)
+        {
+            s.bin_start = s.bin_count + nb;
+            s.item_start = s.bin_start + nb + 1;
+            s.totals = s.item_start + nb + 1;
+        }
+        SDP_HIP_CHECK(hipHostMalloc((void**)&s.totals_host,
+                2 * sizeof(uint32_t), hipHostMallocDefault), status);
+    }
+    ensure_scratch(plan,
+            (int64_t)plan->num_rows * plan->num_chan, status);
+    plan->fft = sdp_fft::create_2d(plan->grid_size, plan->grid_size,
+            plan->is_double != 0, status);
+    if (*status)
+    {
+        if (*status == SDP_ERR_RUNTIME) *status = SDP_ERR_MEM_ALLOC_FAILURE;
+        sdp_gridder_uvw_es_fft_free_plan(plan);
+        return nullptr;
+    }
+    return plan;
+}
+
+void sdp_grid_uvw_es_fft(sdp_GridderUvwEsFft* plan, const sdp_Mem* uvw,
+        const sdp_Mem* freq_hz, const sdp_Mem* vis, const sdp_Mem* weight,
+        sdp_Mem* dirty_image, sdp_Error* status)
+{
+    SDP_LOG_DEBUG("Executing sdp_GridderUvwEsFft...");
+    if (*status || !plan) return;
+    check_parameters(plan->pixsize_x_rad, plan->pixsize_y_rad, status);
+    check_buffers(uvw, freq_hz, vis, weight, dirty_image, false, status);
+    if (*status) return;
+    // Device pointers (fails with SDP_ERR_MEM_LOCATION for host memory).
+    const void* p_uvw = sdp_mem_gpu_buffer_const(uvw, status);
+    const void* p_freq = sdp_mem_gpu_buffer_const(freq_hz, status);
+    const void* p_vis = sdp_mem_gpu_buffer_const(vis, status);
+    const void* p_wt = sdp_mem_gpu_buffer_const(weight, status);
+    void* p_dirty = sdp_mem_gpu_buffer(dirty_image, status);
+    if (*status) return;
+    if (sdp_mem_shape_dim(dirty_image, 0) != plan->image_size ||
+            (int)sdp_mem_is_double(vis) != plan->is_double)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Buffers do not match those used to create the plan");
+        return;
+    }
+    const int64_t rows = sdp_mem_shape_dim(vis, 0);
+    const int chan = (int)sdp_mem_shape_dim(vis, 1);
+    timing_begin(plan);
+    if (plan->is_double)
+        run_grid<double>(plan, rows, chan, *(const double* const*)p_uvw,
+                *(const double* const*)p_freq, *(const double* const*)p_vis,
+                *(const double* const*)p_wt, *(double**)p_dirty, status);
+    else
+        run_grid<float>(plan, rows, chan, *(const float* const*)p_uvw,
+                *(const float* const*)p_freq, *(const float* const*)p_vis,
+                *(const float* const*)p_wt, *(float**)p_dirty, status);
+    timing_end(plan, 0.0);
+}
+
+void sdp_ifft_degrid_uvw_es(sdp_GridderUvwEsFft* plan, const sdp_Mem* uvw,
+        const sdp_Mem* freq_hz, sdp_Mem* vis, const sdp_Mem* weight,
+        sdp_Mem* dirty_image, sdp_Error* status)
+{
+    SDP_LOG_DEBUG("Executing sdp_GridderUvwEsFft...");
+    if (*status || !plan) return;
+    check_parameters(plan->pixsize_x_rad, plan->pixsize_y_rad, status);
+    check_buffers(uvw, freq_hz, vis, weight, dirty_image, true, status);
+    if (*status) return;
+    const void* p_uvw = sdp_mem_gpu_buffer_const(uvw, status);
+    const void* p_freq = sdp_mem_gpu_buffer_const(freq_hz, status);
+    void* p_vis = sdp_mem_gpu_buffer(vis, status);
+    (void)sdp_mem_gpu_buffer_const(weight, status);
+    void* p_dirty = sdp_mem_gpu_buffer(dirty_image, status);
+    if (*status) return;
+    if (sdp_mem_shape_dim(dirty_image, 0) != plan->image_size ||
+            (int)sdp_mem_is_double(vis) != plan->is_double)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Buffers do not match those used to create the plan");
+        return;
+    }
+    const int64_t rows = sdp_mem_shape_dim(vis, 0);
+    const int chan = (int)sdp_mem_shape_dim(vis, 1);
+    timing_begin(plan);
+    if (plan->is_double)
+        run_degrid<double>(plan, rows, chan, *(const double* const*)p_uvw,
+                *(const double* const*)p_freq, *(double**)p_vis,
+                *(double**)p_dirty, status);
+    else
+        run_degrid<float>(plan, rows, chan, *(const float* const*)p_uvw,
+                *(const float* const*)p_freq, *(float**)p_vis,
+                *(float**)p_dirty, status);
+    timing_end(plan, 0.0);
+}
+
+void sdp_gridder_uvw_es_fft_params_from_epsilon(double epsilon,
+        int image_size, int is_double, int* grid_size, int* support,
+        double* beta_over_support)
+{
+    sdp_es::params_from_epsilon(epsilon, image_size, is_double != 0,
+            grid_size, support, beta_over_support);
+}
+
+int sdp_gridder_uvw_es_fft_grid_size(const sdp_GridderUvwEsFft* plan)
+{
+    return plan ? plan->grid_size : 0;
+}
+
+int sdp_gridder_uvw_es_fft_support(const sdp_GridderUvwEsFft* plan)
+{
+    return plan ? plan->support : 0;
+}
+
+int sdp_gridder_uvw_es_fft_num_w_planes(const sdp_GridderUvwEsFft* plan)
+{
+    return plan ? plan->num_total_w_grids : 0;
+}
+
+double sdp_gridder_uvw_es_fft_beta(const sdp_GridderUvwEsFft* plan)
+{
+    return plan ? plan->beta : 0.0;
+}
+
+void sdp_gridder_uvw_es_fft_set_stream(sdp_GridderUvwEsFft* plan,
+        void* hip_stream)
+{
+    if (plan) plan->stream = (hipStream_t)hip_stream;
+}
+
+void sdp_gridder_uvw_es_fft_enable_timing(sdp_GridderUvwEsFft* plan,
+        int enable)
+{
+    if (!plan || (enable != 0) == (plan->timing != 0)) return;
+    for (int k = 0; k < 5; ++k)
+    {
+        if (enable) (void)hipEventCreate(&plan->ev[k]);
+        else (void)hipEventDestroy(plan->ev[k]);
+    }
+    plan->timing = enable ? 1 : 0;
+    plan->have_timing = 0;
+}
+
+int sdp_gridder_uvw_es_fft_get_timing(sdp_GridderUvwEsFft* plan,
+        double* out_ms, int max_values)
+{
+    if (!plan || !plan->timing || !plan->have_timing) return 0;
+    double total = 0.0;
+    for (int k = 0; k < 4; ++k) total += plan->acc_ms[k];
+    plan->acc_ms[4] = total;
+    const int n = max_values < 5 ? max_values : 5;
+    for (int k = 0; k < n; ++k) out_ms[k] = plan->acc_ms[k];
+    return n;
+}
+
+void sdp_grid_uvw_es_fft_scatter(sdp_GridderUvwEsFft* plan,
+        const sdp_Mem* uvw, const sdp_Mem* freq_hz, const sdp_Mem* vis,
+        const sdp_Mem* weight, sdp_Mem* grid, sdp_Error* status)
+{
+    if (*status || !plan) return;
+    if (plan->do_wstacking)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Split gridding is only available for 2-D plans");
+        return;
+    }
+    // Reuse the standard checks with the grid standing in for the image.
+    check_buffers(uvw, freq_hz, vis, weight, nullptr, false, status);
+    if (*status) return;
+    const int64_t G = plan->grid_size;
+    const sdp_MemType gt = plan->is_double ? SDP_MEM_COMPLEX_DOUBLE :
+            SDP_MEM_COMPLEX_FLOAT;
+    if (sdp_mem_type(grid) != gt || sdp_mem_num_dims(grid) != 2 ||
+            sdp_mem_shape_dim(grid, 0) != G || sdp_mem_shape_dim(grid, 1) != G ||
+            !sdp_mem_is_c_contiguous(grid))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("grid must be a contiguous %lld x %lld complex array "
+                "of the plan's precision", (long long)G, (long long)G);
+        return;
+    }
+    const void* p_uvw = sdp_mem_gpu_buffer_const(uvw, status);
+    const void* p_freq = sdp_mem_gpu_buffer_const(freq_hz, status);
+    const void* p_vis = sdp_mem_gpu_buffer_const(vis, status);
+    const void* p_wt = sdp_mem_gpu_buffer_const(weight, status);
+    void* p_grid = sdp_mem_gpu_buffer(grid, status);
+    if (*status) return;
+    const int64_t rows = sdp_mem_shape_dim(vis, 0);
+    const int chan = (int)sdp_mem_shape_dim(vis, 1);
+    ensure_scratch(plan, rows * chan, status);
+    timing_begin(plan);
+    if (plan->is_double)
+        scatter_plane<double>(plan, 0, rows, chan,
+                *(const double* const*)p_uvw, *(const double* const*)p_freq,
+                *(const double* const*)p_vis, *(const double* const*)p_wt,
+                *(double**)p_grid, status);
+    else
+        scatter_plane<float>(plan, 0, rows, chan,
+                *(const float* const*)p_uvw, *(const float* const*)p_freq,
+                *(const float* const*)p_vis, *(const float* const*)p_wt,
+                *(float**)p_grid, status);
+}
+
+void sdp_grid_uvw_es_fft_finish(sdp_GridderUvwEsFft* plan, sdp_Mem* grid,
+        sdp_Mem* dirty_image, sdp_Error* status)
+{
+    if (*status || !plan) return;
+    if (plan->do_wstacking)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Split gridding is only available for 2-D plans");
+        return;
+    }
+    const int64_t G = plan->grid_size;
+    const sdp_MemType gt = plan->is_double ? SDP_MEM_COMPLEX_DOUBLE :
+            SDP_MEM_COMPLEX_FLOAT;
+    const sdp_MemType it = plan->is_double ? SDP_MEM_DOUBLE : SDP_MEM_FLOAT;
+    if (sdp_mem_type(grid) != gt || sdp_mem_shape_dim(grid, 0) != G ||
+            sdp_mem_shape_dim(grid, 1) != G || !sdp_mem_is_c_contiguous(grid) ||
+            sdp_mem_type(dirty_image) != it ||
+            sdp_mem_shape_dim(dirty_image, 0) != plan->image_size ||
+            sdp_mem_shape_dim(dirty_image, 1) != plan->image_size ||
+            !sdp_mem_is_c_contiguous(dirty_image))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("grid / dirty_image do not match the plan");
+        return;
+    }
+    void* p_grid = sdp_mem_gpu_buffer(grid, status);
+    void* p_dirty = sdp_mem_gpu_buffer(dirty_image, status);
+    if (*status) return;
+    sdp_fft::exec_2d(plan->fft, *(void**)p_grid, false, plan->stream, status);
+    if (*status) return;
+    int e = 0;
+    if (plan->is_double)
+        e = sdp_es::screen_corr_2d<double>(image_params<double>(plan),
+                *(double**)p_grid, *(double**)p_dirty, plan->stream);
+    else
+        e = sdp_es::screen_corr_2d<float>(image_params<float>(plan),
+                *(float**)p_grid, *(float**)p_dirty, plan->stream);
+    if (e) *status = (sdp_Error)e;
+}
+
+} // extern "C"
