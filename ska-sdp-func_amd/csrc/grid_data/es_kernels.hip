@@ -352,8 +352,94 @@ __global__ __launch_bounds__(kThreads) void k_zero_shared_tiles(int G,
     }
 }
 
-// Grid mode: one workgroup per work item. Tile accumulated in LDS (planar
-// re / im, row stride 72), written to HBM once.
+// Wave-uniform broadcast of lane j's value (v_readlane -> SGPR).
+__device__ __forceinline__ int lane_bcast(int x, int j)
+{
+    return __builtin_amdgcn_readlane(x, j);
+}
+__device__ __forceinline__ float lane_bcast(float x, int j)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j));
+}
+__device__ __forceinline__ double lane_bcast(double x, int j)
+{
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), j);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// One batch of up to 64 bucketed records, one per lane, with the per-entry
+// tap window (relative to the tile) packed for wave-uniform decoding:
+//   win = lo_u | (hi_u + 1) << 8 | lo_v << 16 | (hi_v + 1) << 24
+//   org = (u0 - tu0 + 256) | (v0 - tv0 + 256) << 16
+// where lo/hi are tap offsets from the entry's first tap u0 / v0 that lie
+// inside [tile, tile + kTile) (the whole window in gather mode).
+template<typename T>
+struct Batch
+{
+    T pu, pv, a, b, kw;
+    int u0, v0;
+    int win, org;
+    uint64_t wide;   // entries with more than 8 taps on an axis
+    int cnt;
+};
+
+template<typename T, bool DO_W, int WORDS>
+__device__ __forceinline__ void load_batch(const EsParams<T>& p,
+        const T* __restrict__ recs, uint32_t base, uint32_t end, int lane,
+        int tu0, int tv0, int clip_rows, Batch<T>& bt)
+{
+    bt.cnt = (int)min(64u, end - base);
+    bt.pu = T(0);
+    bt.pv = T(0);
+    bt.a = T(0);
+    bt.b = T(0);
+    bt.kw = T(1);
+    if (lane < bt.cnt)
+    {
+        const T* r = recs + (size_t)(base + lane) * WORDS;
+        bt.pu = r[0];
+        bt.pv = r[1];
+        bt.a = r[2];
+        bt.b = r[3];
+        if (DO_W) bt.kw = r[4];
+    }
+    int u1, v1;
+    tap_range(p, bt.pu, bt.pv, bt.u0, u1, bt.v0, v1);
+    const int lo_u = max(bt.u0, tu0) - bt.u0;
+    const int hi_u = min(u1, tu0 + clip_rows - 1) - bt.u0;
+    const int lo_v = max(bt.v0, tv0) - bt.v0;
+    const int hi_v = min(v1, tv0 + clip_rows - 1) - bt.v0;
+    bt.win = lo_u | ((hi_u + 1) << 8) | (lo_v << 16) | ((hi_v + 1) << 24);
+    bt.org = (bt.u0 - tu0 + 256) | ((bt.v0 - tv0 + 256) << 16);
+    bt.wide = __ballot(lane < bt.cnt && (u1 - bt.u0 > 7 || v1 - bt.v0 > 7));
+}
+
+// Cooperative ES taps for entries g..g+3 of a batch: lane L evaluates tap
+// (L & 7) of axis (L >> 3) & 1 (0 = u, 1 = v) of entry g + (L >> 4), with
+// exactly the reference's arithmetic for grid coordinate u0 + t.
+template<typename T>
+__device__ __forceinline__ T group_taps(const EsParams<T>& p,
+        const Batch<T>& bt, int g, int lane, T inv_hs)
+{
+    // (A shuffle returns the SOURCE lane's value, so fetch both axes and
+    // select on the reading side.)
+    const int jsel = g + (lane >> 4);
+    const bool axis_v = (lane >> 3) & 1;
+    const T pu = __shfl(bt.pu, jsel), pv = __shfl(bt.pv, jsel);
+    const int u0 = __shfl(bt.u0, jsel), v0 = __shfl(bt.v0, jsel);
+    const T ps = axis_v ? pv : pu;
+    const int ss = axis_v ? v0 : u0;
+    return es_tap(p.beta, ((T)(ss + (lane & 7)) - ps) * inv_hs);
+}
+
+// Grid mode: one workgroup per work item. The tile is accumulated in LDS
+// (planar re / im, row stride 72: the 8x8 tap block of a wave is
+// bank-conflict free) and written to HBM once.
+// Per wave: records are loaded 64 at a time (one per lane, coalesced); the
+// 16 taps of four entries are evaluated by the 64 lanes together, then each
+// entry is applied by the whole wave, lane = (du, dv) tap, two ds_add_f32.
 template<typename T, bool DO_W>
 __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
         const T* __restrict__ recs, const uint32_t* __restrict__ bin_start,
@@ -382,27 +468,62 @@ __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int du = lane >> 3, dv = lane & 7;
-    for (uint32_t e = e0 + wave; e < e1; e += kWaves)
+    const int lane_off = du * S + dv;
+    const int lane_par = (du + dv) & 1;
+    const T inv_hs = T(1) / (T(p.support) / T(2));
+    for (uint32_t base = e0 + wave * 64; base < e1; base += kWaves * 64)
     {
-        const T* rec = recs + (size_t)e * kWords;
-        const T pu = rec[0], pv = rec[1], vre = rec[2], vim = rec[3];
-        const T kw = DO_W ? rec[4] : T(1);
-        int u0, u1, v0, v1;
-        tap_range(p, pu, pv, u0, u1, v0, v1);
-        // Only the taps inside this tile.
-        u0 = max(u0, tu0);
-        u1 = min(u1, tu0 + kTile - 1);
-        v0 = max(v0, tv0);
-        v1 = min(v1, tv0 + kTile - 1);
-        for (int ub = u0; ub <= u1; ub += 8)
+        Batch<T> bt;
+        load_batch<T, DO_W, kWords>(p, recs, base, e1, lane, tu0, tv0, kTile,
+                bt);
+        for (int g = 0; g < bt.cnt; g += 4)
         {
-            for (int vb = v0; vb <= v1; vb += 8)
+            const T es = group_taps(p, bt, g, lane, inv_hs);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
             {
-                const int u = ub + du, v = vb + dv;
-                if (u <= u1 && v <= v1)
+                const int j = g + jj;
+                if (j >= bt.cnt) break;
+                const T ku = __shfl(es, (jj << 4) | du);
+                const T kv = __shfl(es, (jj << 4) | 8 | dv);
+                const T vre = lane_bcast(bt.a, j), vim = lane_bcast(bt.b, j);
+                const T kw = DO_W ? lane_bcast(bt.kw, j) : T(1);
+                if ((bt.wide >> j) & 1ull)
                 {
-                    const T k = tap_weight(p, u, v, pu, pv, kw);
-                    const int a = (u - tu0) * S + (v - tv0);
+                    // Rare: a tap exactly on +-W/2 gives W+1 taps on an
+                    // axis. Generic per-lane loop over the tile window.
+                    const T pu = lane_bcast(bt.pu, j), pv = lane_bcast(bt.pv, j);
+                    int u0, u1, v0, v1;
+                    tap_range(p, pu, pv, u0, u1, v0, v1);
+                    u0 = max(u0, tu0);
+                    u1 = min(u1, tu0 + kTile - 1);
+                    v0 = max(v0, tv0);
+                    v1 = min(v1, tv0 + kTile - 1);
+                    for (int ub = u0; ub <= u1; ub += 8)
+                        for (int vb = v0; vb <= v1; vb += 8)
+                        {
+                            const int u = ub + du, v = vb + dv;
+                            if (u <= u1 && v <= v1)
+                            {
+                                const T k = tap_weight(p, u, v, pu, pv, kw);
+                                const int a = (u - tu0) * S + (v - tv0);
+                                atomicAdd(&s_re[a], vre * k);
+                                atomicAdd(&s_im[a], vim * k);
+                            }
+                        }
+                    continue;
+                }
+                const int win = lane_bcast(bt.win, j);
+                const int org = lane_bcast(bt.org, j);
+                const bool act = du >= (win & 255) && du < ((win >> 8) & 255) &&
+                        dv >= ((win >> 16) & 255) && dv < (win >> 24);
+                T k = ku * kv;
+                if (DO_W) k *= kw;
+                if ((lane_par + org + (org >> 16)) & 1) k = -k;
+                if (act)
+                {
+                    const int a = lane_off + ((org & 0xffff) - 256) * S +
+                            ((org >> 16) - 256);
                     atomicAdd(&s_re[a], vre * k);
                     atomicAdd(&s_im[a], vim * k);
                 }
@@ -422,7 +543,7 @@ __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
             const int r = k / kPerRow, c = (k - r * kPerRow) * kCells;
             if (r >= nr || c >= nc) continue;
             T* dst = grid + ((size_t)(r0 + r) * p.G + c0 + c) * 2;
-            if (kCells == 2)
+            if constexpr (kCells == 2)
             {
                 float4 v;
                 v.x = (float)s_re[r * S + c];
@@ -456,9 +577,146 @@ __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
     }
 }
 
+// Grid mode, f32, matrix-core form (the hot path).
+//
+// A tile's grid is a sum of rank-1 outer products,
+//   grid[u][v] += sum_k (s_u ku_k[u]) * (s_v kv_k[v] w_k V_k)
+// (s_u s_v = (-1)^(u+v) checkerboard, separable), i.e. C += A B with
+// A[u][k] = taps along u of entry k and B[k][v] = taps along v times the
+// weighted visibility. A workgroup of 16 waves owns a 64x64 tile; wave w
+// keeps the 16x16 sub-tile (w>>2, w&3) in 2 x 4 accumulator registers
+// (re / im) and applies FOUR entries per v_mfma_f32_16x16x4_f32: lane l
+// evaluates A[l&15][l>>4] and B[l>>4][l&15], i.e. one u-tap and one v-tap,
+// with exactly the reference's tap arithmetic. No LDS atomics, no
+// per-cell read-modify-write: the sub-tile leaves the registers once.
+// Entries are staged in LDS 1024 at a time; each wave scans them 64 at a
+// time (ballot of entries whose taps overlap its sub-tile) and walks the
+// set bits four at a time on the scalar unit.
+template<bool DO_W>
+__global__ __launch_bounds__(1024) void k_scatter_mfma(EsParams<float> p,
+        const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
+        const uint32_t* __restrict__ item_start, float* __restrict__ grid)
+{
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int kChunk = 1024;
+    constexpr int kVec = DO_W ? 2 : 1;   // float4s per record
+    __shared__ float4 s_rec[kChunk * kVec];
+
+    const uint32_t item = blockIdx.x;
+    const int b = find_bin(item_start, p.nbins, item);
+    const uint32_t piece = item - item_start[b];
+    const uint32_t npieces = item_start[b + 1] - item_start[b];
+    const uint32_t e0 = bin_start[b] + piece * kPiece;
+    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
+    const int half = p.G / 2;
+    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int sub_r = (wave >> 2) * 16, sub_c = (wave & 3) * 16;
+    const int su0 = r0 - half + sub_r, sv0 = c0 - half + sub_c;
+    const int i = lane & 15, kq = lane >> 4;
+    const int my_u = su0 + i;            // A row  (grid u of this lane)
+    const int my_v = sv0 + i;            // B col  (grid v of this lane)
+    const float sgn_u = (my_u & 1) ? -1.0f : 1.0f;
+    const float sgn_v = (my_v & 1) ? -1.0f : 1.0f;
+    const float inv_hs = 1.0f / ((float)p.support / 2.0f);
+    f32x4 acc_re = {0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 acc_im = {0.0f, 0.0f, 0.0f, 0.0f};
+    const float4* recs4 = (const float4*)recs;
+
+    for (uint32_t cb = e0; cb < e1; cb += kChunk)
+    {
+        const int n = (int)min((uint32_t)kChunk, e1 - cb);
+        __syncthreads();
+        for (int k = threadIdx.x; k < n * kVec; k += 1024)
+            s_rec[k] = recs4[(size_t)cb * kVec + k];
+        __syncthreads();
+        for (int bb = 0; bb < n; bb += 64)
+        {
+            const int cnt = min(64, n - bb);
+            bool hit = false;
+            if (lane < cnt)
+            {
+                const float4 r = s_rec[(bb + lane) * kVec];
+                int u0, u1, v0, v1;
+                tap_range(p, r.x, r.y, u0, u1, v0, v1);
+                hit = u1 >= su0 && u0 <= su0 + 15 && v1 >= sv0 &&
+                        v0 <= sv0 + 15;
+            }
+            uint64_t mask = __ballot(hit);
+            while (mask)
+            {
+                // Next (up to) four entries on the scalar unit.
+                int sel[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                {
+                    if (mask)
+                    {
+                        sel[q] = (int)__builtin_ctzll(mask);
+                        mask &= mask - 1;
+                    }
+                    else
+                    {
+                        sel[q] = -1;
+                    }
+                }
+                const int mine = kq == 0 ? sel[0] : kq == 1 ? sel[1] :
+                        kq == 2 ? sel[2] : sel[3];
+                float a = 0.0f, bre = 0.0f, bim = 0.0f;
+                if (mine >= 0)
+                {
+#pragma clang fp contract(off)
+                    const float4 r = s_rec[(bb + mine) * kVec];
+                    int u0, u1, v0, v1;
+                    tap_range(p, r.x, r.y, u0, u1, v0, v1);
+                    if (my_u >= u0 && my_u <= u1)
+                        a = sgn_u * es_tap(p.beta,
+                                ((float)my_u - r.x) * inv_hs);
+                    if (my_v >= v0 && my_v <= v1)
+                    {
+                        float kv = sgn_v * es_tap(p.beta,
+                                ((float)my_v - r.y) * inv_hs);
+                        if (DO_W) kv *= s_rec[(bb + mine) * kVec + 1].x;
+                        bre = kv * r.z;
+                        bim = kv * r.w;
+                    }
+                }
+                acc_re = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bre, acc_re,
+                        0, 0, 0);
+                acc_im = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bim, acc_im,
+                        0, 0, 0);
+            }
+        }
+    }
+
+    // C/D layout of 16x16x4 f32: col = lane & 15, row = (lane >> 4)*4 + r.
+    const int col = c0 + sub_c + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const int row = r0 + sub_r + kq * 4 + r;
+        if (row >= p.G || col >= p.G) continue;
+        float* dst = grid + ((size_t)row * p.G + col) * 2;
+        if (npieces == 1)
+        {
+            float2 v;
+            v.x = acc_re[r];
+            v.y = acc_im[r];
+            *(float2*)dst = v;
+        }
+        else
+        {
+            if (acc_re[r] != 0.0f) unsafeAtomicAdd(dst, acc_re[r]);
+            if (acc_im[r] != 0.0f) unsafeAtomicAdd(dst + 1, acc_im[r]);
+        }
+    }
+}
+
 // Degrid mode: one workgroup per work item; the tile plus its support halo
-// is staged in LDS once, then each wave gathers one visibility at a time
-// (lane = tap) and reduces across the wave.
+// is staged in LDS once. Records are loaded 64 per wave; taps of four
+// entries are evaluated cooperatively; each entry is gathered by the whole
+// wave (lane = tap) and reduced with a butterfly; lane j keeps entry j's sum
+// so the batch's visibilities are updated by one scattered RMW per lane.
 template<typename T, bool DO_W>
 __global__ __launch_bounds__(kThreads) void k_gather(EsParams<T> p,
         const T* __restrict__ recs, const uint32_t* __restrict__ bin_start,
@@ -494,40 +752,83 @@ __global__ __launch_bounds__(kThreads) void k_gather(EsParams<T> p,
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int du = lane >> 3, dv = lane & 7;
-    for (uint32_t e = e0 + wave; e < e1; e += kWaves)
+    const int lane_off = du * ws + dv;
+    const int lane_par = (du + dv) & 1;
+    const T inv_hs = T(1) / (T(p.support) / T(2));
+    for (uint32_t base = e0 + wave * 64; base < e1; base += kWaves * 64)
     {
-        const T* rec = recs + (size_t)e * 4;
-        const T pu = rec[0], pv = rec[1], kwf = rec[2];
-        const T kw = fabs(kwf);
-        int u0, u1, v0, v1;
-        tap_range(p, pu, pv, u0, u1, v0, v1);
-        T acc_re = T(0), acc_im = T(0);
-        for (int ub = u0; ub <= u1; ub += 8)
+        Batch<T> bt;
+        // Gather records are {pu, pv, kw*flip, index}: kw = |a|.
+        load_batch<T, false, 4>(p, recs, base, e1, lane, tu0, tv0, wrows, bt);
+        const T kw_lane = fabs(bt.a);
+        T res_re = T(0), res_im = T(0);
+        for (int g = 0; g < bt.cnt; g += 4)
         {
-            for (int vb = v0; vb <= v1; vb += 8)
+            const T es = group_taps(p, bt, g, lane, inv_hs);
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj)
             {
-                const int u = ub + du, v = vb + dv;
-                if (u <= u1 && v <= v1)
+                const int j = g + jj;
+                if (j >= bt.cnt) break;
+                const T ku = __shfl(es, (jj << 4) | du);
+                const T kv = __shfl(es, (jj << 4) | 8 | dv);
+                const T kw = DO_W ? lane_bcast(kw_lane, j) : T(1);
+                T acc_re = T(0), acc_im = T(0);
+                if ((bt.wide >> j) & 1ull)
                 {
-                    const T k = tap_weight(p, u, v, pu, pv, kw);
-                    const int a = (u - tu0) * ws + (v - tv0);
-                    acc_re += w_re[a] * k;
-                    acc_im += w_im[a] * k;
+                    const T pu = lane_bcast(bt.pu, j), pv = lane_bcast(bt.pv, j);
+                    int u0, u1, v0, v1;
+                    tap_range(p, pu, pv, u0, u1, v0, v1);
+                    for (int ub = u0; ub <= u1; ub += 8)
+                        for (int vb = v0; vb <= v1; vb += 8)
+                        {
+                            const int u = ub + du, v = vb + dv;
+                            if (u <= u1 && v <= v1)
+                            {
+                                const T k = tap_weight(p, u, v, pu, pv, kw);
+                                const int a = (u - tu0) * ws + (v - tv0);
+                                acc_re += w_re[a] * k;
+                                acc_im += w_im[a] * k;
+                            }
+                        }
+                }
+                else
+                {
+                    const int win = lane_bcast(bt.win, j);
+                    const int org = lane_bcast(bt.org, j);
+                    const bool act = du >= (win & 255) &&
+                            du < ((win >> 8) & 255) &&
+                            dv >= ((win >> 16) & 255) && dv < (win >> 24);
+                    T k = ku * kv;
+                    if (DO_W) k *= kw;
+                    if ((lane_par + org + (org >> 16)) & 1) k = -k;
+                    if (act)
+                    {
+                        const int a = lane_off + ((org & 0xffff) - 256) * ws +
+                                ((org >> 16) - 256);
+                        acc_re = w_re[a] * k;
+                        acc_im = w_im[a] * k;
+                    }
+                }
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1)
+                {
+                    acc_re += __shfl_xor(acc_re, off);
+                    acc_im += __shfl_xor(acc_im, off);
+                }
+                if (lane == j)
+                {
+                    res_re = acc_re;
+                    res_im = acc_im;
                 }
             }
         }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1)
+        if (lane < bt.cnt)
         {
-            acc_re += __shfl_xor(acc_re, off);
-            acc_im += __shfl_xor(acc_im, off);
-        }
-        if (lane == 0)
-        {
-            const uint64_t i = bits_idx(rec[3]);
-            const T flip = signbit(kwf) ? T(-1) : T(1);
-            vis[2 * i] += acc_re;
-            vis[2 * i + 1] += acc_im * flip;   // kernels.cu:267-268
+            const uint64_t i = bits_idx(bt.b);
+            const T flip = signbit(bt.a) ? T(-1) : T(1);
+            vis[2 * i] += res_re;
+            vis[2 * i + 1] += res_im * flip;   // kernels.cu:267-268
         }
     }
 }
@@ -679,6 +980,20 @@ __global__ void k_reverse_screen(ImageParams<T> ip, int plane,
     g[1] = im;
 }
 
+// hipFuncSetAttribute is a host call with real latency: do it once per
+// kernel instantiation, not per launch (it would otherwise leave the GPU
+// idle between the bucketing and the tile kernel).
+template<auto Kernel>
+int allow_lds(size_t bytes)
+{
+    static int done_bytes = 0;   // one per kernel instantiation
+    if ((int)bytes <= done_bytes) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute((const void*)Kernel,
+            hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) done_bytes = (int)bytes;
+    return e;
+}
+
 dim3 image_blocks(int n)
 {
     return dim3((unsigned)((n + 63) / 64), (unsigned)((n + 3) / 4));
@@ -766,18 +1081,27 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
             p.G, p.ntiles, s.item_start, grid);
     SDP_HIP_CHECK_LAUNCH(status);
+    if constexpr (sizeof(T) == 4)
+    {
+        if (p.do_w)
+            k_scatter_mfma<true><<<n_items, 1024, 0, stream>>>(
+                    p, (const float*)s.recs, s.bin_start, s.item_start, grid);
+        else
+            k_scatter_mfma<false><<<n_items, 1024, 0, stream>>>(
+                    p, (const float*)s.recs, s.bin_start, s.item_start, grid);
+        SDP_HIP_CHECK_LAUNCH(status);
+        return *status;
+    }
     const size_t lds = 2 * (size_t)kTile * kScatterStride * sizeof(T);
     if (p.do_w)
     {
-        SDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter<T, true>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), status);
+        SDP_HIP_CHECK(((hipError_t)allow_lds<k_scatter<T, true>>(lds)), status);
         k_scatter<T, true><<<n_items, kThreads, lds, stream>>>(
                 p, (const T*)s.recs, s.bin_start, s.item_start, grid);
     }
     else
     {
-        SDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_scatter<T, false>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), status);
+        SDP_HIP_CHECK(((hipError_t)allow_lds<k_scatter<T, false>>(lds)), status);
         k_scatter<T, false><<<n_items, kThreads, lds, stream>>>(
                 p, (const T*)s.recs, s.bin_start, s.item_start, grid);
     }
@@ -802,16 +1126,14 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     }
     if (p.do_w)
     {
-        SDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_gather<T, true>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), status);
+        SDP_HIP_CHECK(((hipError_t)allow_lds<k_gather<T, true>>(lds)), status);
         k_gather<T, true><<<n_items, kThreads, lds, stream>>>(p,
                 (const T*)s.recs, s.bin_start, s.item_start, grid, vis, wrows,
                 ws);
     }
     else
     {
-        SDP_HIP_CHECK(hipFuncSetAttribute((const void*)k_gather<T, false>,
-                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), status);
+        SDP_HIP_CHECK(((hipError_t)allow_lds<k_gather<T, false>>(lds)), status);
         k_gather<T, false><<<n_items, kThreads, lds, stream>>>(p,
                 (const T*)s.recs, s.bin_start, s.item_start, grid, vis, wrows,
                 ws);

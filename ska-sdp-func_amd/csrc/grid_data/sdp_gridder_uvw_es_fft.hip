@@ -203,8 +203,10 @@ void timing_mark(sdp_GridderUvwEsFft* plan, int k)
     if (plan->timing) (void)hipEventRecord(plan->ev[k], plan->stream);
 }
 
-// Sum phase times of one plane into acc_ms (syncs the last event).
-void timing_collect(sdp_GridderUvwEsFft* plan)
+// Sum the phase times of one plane into acc_ms (syncs the last event).
+// Interval k (event k -> k+1) is accumulated into slot[k]; slots are
+// 0 bucketing, 1 scatter/gather kernel, 2 FFT, 3 image-plane kernels.
+void timing_collect(sdp_GridderUvwEsFft* plan, const int slot[4])
 {
     if (!plan->timing) return;
     (void)hipEventSynchronize(plan->ev[4]);
@@ -212,9 +214,12 @@ void timing_collect(sdp_GridderUvwEsFft* plan)
     {
         float ms = 0.0f;
         (void)hipEventElapsedTime(&ms, plan->ev[k], plan->ev[k + 1]);
-        plan->acc_ms[k] += ms;
+        plan->acc_ms[slot[k]] += ms;
     }
 }
+
+const int kGridSlots[4] = {0, 1, 2, 3};     // bucket, scatter, fft, screen
+const int kDegridSlots[4] = {0, 3, 2, 1};   // bucket, screen, fft, gather
 
 template<typename T>
 sdp_es::EsParams<T> es_params(const sdp_GridderUvwEsFft* plan, int plane)
@@ -298,7 +303,7 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
         }
         if (e) { *status = (sdp_Error)e; return; }
         timing_mark(plan, 4);
-        timing_collect(plan);
+        timing_collect(plan, kGridSlots);
     }
 }
 
@@ -337,7 +342,7 @@ void run_degrid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
                 plan->stream);
         if (e) { *status = (sdp_Error)e; return; }
         timing_mark(plan, 4);
-        timing_collect(plan);
+        timing_collect(plan, kDegridSlots);
     }
 }
 

@@ -230,3 +230,26 @@ def test_plan_parameters_match_reference_golden(device):
         assert plan.grid_size == p["grid_size"]
         assert plan.support == p["support"]
         assert plan.beta == pytest.approx(p["beta"] * p["support"], rel=1e-15)
+
+
+@pytest.mark.parametrize("rows", [1, 5, 70, 3000])
+def test_scatter_grid_matches_oracle(device, rows):
+    """uv grid after the tile scatter (before the FFT) vs the oracle's."""
+    import torch
+    from ska_sdp_func.grid_data import GridderUvwEsFft
+
+    n = 256
+    uvw, freq, vis, wt, px = make_case(12, rows, 2, n)
+    dirty = torch.zeros((n, n), dtype=torch.float32, device=device)
+    g = [_gpu(a, device) for a in (uvw, freq, vis, wt)]
+    plan = GridderUvwEsFft(*g, dirty, px, px, 1e-5, False)
+    G = plan.grid_size
+    grid = torch.full((G, G), 7.0, dtype=torch.complex64, device=device)
+    plan.grid_scatter(*g, grid)
+    geo = es_oracle.geometry_for(uvw, freq, vis, np.zeros((n, n), np.float32),
+                                 px, 1e-5, False)
+    ref = es_oracle.scatter(geo, uvw, freq, vis, wt)
+    out = grid.cpu().numpy()
+    bad = np.argwhere(np.abs(out - ref) > 2e-6 * np.abs(ref).max())
+    assert len(bad) == 0, (len(bad), bad[:5], out[tuple(bad[0])],
+                           ref[tuple(bad[0])])
