@@ -53,6 +53,8 @@ struct BucketScratch
     uint32_t* bin_start = nullptr;  // [nbins + 1]
     uint32_t* item_start = nullptr; // [nbins + 1]
     uint32_t* totals = nullptr;     // [2]: entries, items
+    uint32_t* item_bin = nullptr;   // [item_capacity]: work item -> bin
+    uint32_t item_capacity = 0;
     uint32_t* totals_host = nullptr;// pinned host mirror of totals
     void* recs = nullptr;           // bucketed records
     size_t recs_bytes = 0;

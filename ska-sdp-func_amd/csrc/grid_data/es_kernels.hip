@@ -33,6 +33,25 @@ __device__ __forceinline__ T es_tap(T beta, T x)
     return (xx > T(1)) ? T(0) : exp(beta * (sqrt(T(1) - xx) - T(1)));
 }
 
+// Exponential of semicircle on the hardware transcendental units, for the
+// f32 matrix-core kernels: v_sqrt_f32 (1 ulp; the argument 1 - x^2 lies in
+// [6e-8, 1], never denormal) and exp(y) = 2^(y log2 e) with the rounding
+// error of y log2 e fed back to first order (|error| ~ 1-2 ulp over the
+// kernel's range |y| <= beta ~ 16). Same formula and branch as es_tap;
+// the taps differ from libm's correctly rounded ones by ~1e-7 relative.
+__device__ __forceinline__ float es_tap_fast(float beta, float x)
+{
+#pragma clang fp contract(off)
+    const float xx = x * x;
+    const float y = beta * (__builtin_amdgcn_sqrtf(1.0f - xx) - 1.0f);
+    const float t = y * 1.44269504088896341f;
+    const float err = __builtin_fmaf(y, 1.44269504088896341f, -t) +
+            y * 1.92596299112661746e-8f;
+    const float e = __builtin_amdgcn_exp2f(t);
+    const float r = __builtin_fmaf(e, err * 0.693147180559945309f, e);
+    return (xx > 1.0f) ? 0.0f : r;
+}
+
 // Tap range of one visibility on the current w-plane (kernels.cu:150-196,
 // 301-347). Returns false if the visibility does not touch the plane.
 template<typename T>
@@ -211,7 +230,8 @@ __global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
 __global__ __launch_bounds__(1024) void k_scan_bins(
         const uint32_t* __restrict__ bin_count, int nbins,
         uint32_t* __restrict__ bin_start, uint32_t* __restrict__ item_start,
-        uint32_t* __restrict__ totals)
+        uint32_t* __restrict__ totals, uint32_t* __restrict__ item_bin,
+        uint32_t item_capacity)
 {
     __shared__ uint32_t s_cnt[1024], s_itm[1024];
     const int t = threadIdx.x;
@@ -240,10 +260,13 @@ __global__ __launch_bounds__(1024) void k_scan_bins(
     for (int b = b0; b < b1; ++b)
     {
         const uint32_t n = bin_count[b];
+        const uint32_t ni = max(1u, (n + kPiece - 1) / kPiece);
         bin_start[b] = run_c;
         item_start[b] = run_i;
+        for (uint32_t k = 0; k < ni; ++k)
+            if (run_i + k < item_capacity) item_bin[run_i + k] = (uint32_t)b;
         run_c += n;
-        run_i += max(1u, (n + kPiece - 1) / kPiece);
+        run_i += ni;
     }
     if (t == 1023)
     {
@@ -321,19 +344,6 @@ __global__ __launch_bounds__(kThreads) void k_bucket_fill(EsParams<T> p,
             for (int k = 0; k < kWords; ++k) dst[k] = rec[k];
         }
     }
-}
-
-// Work item -> (bin, piece). item_start is strictly increasing.
-__device__ __forceinline__ int find_bin(const uint32_t* item_start, int nbins,
-        uint32_t item)
-{
-    int lo = 0, hi = nbins;
-    while (hi - lo > 1)
-    {
-        const int mid = (lo + hi) >> 1;
-        if (item_start[mid] <= item) lo = mid; else hi = mid;
-    }
-    return lo;
 }
 
 // Zero the grid cells of tiles that several work items share.
@@ -443,7 +453,8 @@ __device__ __forceinline__ T group_taps(const EsParams<T>& p,
 template<typename T, bool DO_W>
 __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
         const T* __restrict__ recs, const uint32_t* __restrict__ bin_start,
-        const uint32_t* __restrict__ item_start, T* __restrict__ grid)
+        const uint32_t* __restrict__ item_start,
+        const uint32_t* __restrict__ item_bin, T* __restrict__ grid)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int S = kScatterStride;
@@ -456,7 +467,7 @@ __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
         s_im[k] = T(0);
     }
     const uint32_t item = blockIdx.x;
-    const int b = find_bin(item_start, p.nbins, item);
+    const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
     const uint32_t npieces = item_start[b + 1] - item_start[b];
     const uint32_t e0 = bin_start[b] + piece * kPiece;
@@ -592,122 +603,345 @@ __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
 // Entries are staged in LDS 1024 at a time; each wave scans them 64 at a
 // time (ballot of entries whose taps overlap its sub-tile) and walks the
 // set bits four at a time on the scalar unit.
+// Staging of one chunk of bucketed entries into per-sub-tile visit lists
+// (a pool in LDS): thread t classifies entry t by the sub-tiles (a
+// kSub x kSub grid of 16x16 cells starting at the tile origin) its taps
+// touch, counts with one ballot per sub-tile, and after a prefix over the
+// counts writes the entry's 16-byte record once per sub-tile it touches.
+template<int kSub>
+struct VisitPool
+{
+    uint32_t count[kSub * kSub];
+    uint32_t offset[kSub * kSub + 1];
+};
+
+template<int kSub>
+__device__ __forceinline__ void pool_classify(VisitPool<kSub>& vp, int lane,
+        int wlo_r, int whi_r, int wlo_c, int whi_c, int pos[4], int sub[4])
+{
+    int nh = 0;
+#pragma unroll
+    for (int st = 0; st < kSub * kSub; ++st)
+    {
+        const int sr = st / kSub, sc = st % kSub;
+        const bool hit = sr >= wlo_r && sr <= whi_r && sc >= wlo_c &&
+                sc <= whi_c;
+        const uint64_t m = __ballot(hit);
+        if (!m) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&vp.count[st], (uint32_t)__popcll(m));
+        base = __shfl(base, 0);
+        if (hit && nh < 4)
+        {
+            pos[nh] = (int)(base + __popcll(m & ((1ull << lane) - 1ull)));
+            sub[nh] = st;
+            ++nh;
+        }
+    }
+    for (int k = nh; k < 4; ++k) sub[k] = -1;
+}
+
+template<int kSub>
+__device__ __forceinline__ void pool_prefix(VisitPool<kSub>& vp)
+{
+    if (threadIdx.x == 0)
+    {
+        uint32_t run = 0;
+        for (int st = 0; st < kSub * kSub; ++st)
+        {
+            vp.offset[st] = run;
+            run += vp.count[st];
+        }
+        vp.offset[kSub * kSub] = run;
+    }
+}
+
 template<bool DO_W>
-__global__ __launch_bounds__(1024) void k_scatter_mfma(EsParams<float> p,
+__global__ __launch_bounds__(256) void k_scatter_mfma(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
-        const uint32_t* __restrict__ item_start, float* __restrict__ grid)
+        const uint32_t* __restrict__ item_start,
+        const uint32_t* __restrict__ item_bin, float* __restrict__ grid)
 {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    constexpr int kChunk = 1024;
-    constexpr int kVec = DO_W ? 2 : 1;   // float4s per record
-    __shared__ float4 s_rec[kChunk * kVec];
+    constexpr int kChunk = 256;           // one entry per thread
+    constexpr int kVec = DO_W ? 2 : 1;    // float4s per bucketed record
+    __shared__ float4 s_pool[4 * kChunk]; // {pu, pv, vre, vim} per visit
+    __shared__ VisitPool<4> s_vp;
 
     const uint32_t item = blockIdx.x;
-    const int b = find_bin(item_start, p.nbins, item);
+    const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
     const uint32_t npieces = item_start[b + 1] - item_start[b];
     const uint32_t e0 = bin_start[b] + piece * kPiece;
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
     const int half = p.G / 2;
     const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    const int tu0 = r0 - half, tv0 = c0 - half;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int sub_r = (wave >> 2) * 16, sub_c = (wave & 3) * 16;
-    const int su0 = r0 - half + sub_r, sv0 = c0 - half + sub_c;
     const int i = lane & 15, kq = lane >> 4;
-    const int my_u = su0 + i;            // A row  (grid u of this lane)
-    const int my_v = sv0 + i;            // B col  (grid v of this lane)
+    // This wave owns sub-tiles {wave, wave+4, wave+8, wave+12}: sub-tile
+    // row band (wave) and all four column blocks -> shared A row index.
+    const int sub_r = wave * 16;
+    const int my_u = tu0 + sub_r + i;     // A row: grid u of this lane
+    const float fu = (float)my_u;
     const float sgn_u = (my_u & 1) ? -1.0f : 1.0f;
-    const float sgn_v = (my_v & 1) ? -1.0f : 1.0f;
-    const float inv_hs = 1.0f / ((float)p.support / 2.0f);
-    f32x4 acc_re = {0.0f, 0.0f, 0.0f, 0.0f};
-    f32x4 acc_im = {0.0f, 0.0f, 0.0f, 0.0f};
+    const float hs = (float)p.support / 2.0f;
+    const float inv_hs = 1.0f / hs;
+    f32x4 acc_re[4], acc_im[4];
+#pragma unroll
+    for (int cblk = 0; cblk < 4; ++cblk)
+    {
+        acc_re[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        acc_im[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
     const float4* recs4 = (const float4*)recs;
 
     for (uint32_t cb = e0; cb < e1; cb += kChunk)
     {
         const int n = (int)min((uint32_t)kChunk, e1 - cb);
-        __syncthreads();
-        for (int k = threadIdx.x; k < n * kVec; k += 1024)
-            s_rec[k] = recs4[(size_t)cb * kVec + k];
-        __syncthreads();
-        for (int bb = 0; bb < n; bb += 64)
+        const int t = threadIdx.x;
+        __syncthreads();   // previous chunk consumed
+        if (t < 16) s_vp.count[t] = 0;
+        float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        int wlo_r = 1, whi_r = 0, wlo_c = 1, whi_c = 0;
+        if (t < n)
         {
-            const int cnt = min(64, n - bb);
-            bool hit = false;
-            if (lane < cnt)
+            r = recs4[(size_t)(cb + t) * kVec];
+            if (DO_W)
             {
-                const float4 r = s_rec[(bb + lane) * kVec];
-                int u0, u1, v0, v1;
-                tap_range(p, r.x, r.y, u0, u1, v0, v1);
-                hit = u1 >= su0 && u0 <= su0 + 15 && v1 >= sv0 &&
-                        v0 <= sv0 + 15;
+                const float kw = recs4[(size_t)(cb + t) * kVec + 1].x;
+                r.z *= kw;
+                r.w *= kw;
             }
-            uint64_t mask = __ballot(hit);
-            while (mask)
-            {
-                // Next (up to) four entries on the scalar unit.
-                int sel[4];
+            int u0, u1, v0, v1;
+            tap_range(p, r.x, r.y, u0, u1, v0, v1);
+            wlo_r = max(u0 - tu0, 0) >> 4;
+            whi_r = min(u1 - tu0, kTile - 1) >> 4;
+            wlo_c = max(v0 - tv0, 0) >> 4;
+            whi_c = min(v1 - tv0, kTile - 1) >> 4;
+        }
+        __syncthreads();   // counters zeroed
+        int pos[4], sub[4];
+        pool_classify<4>(s_vp, lane, wlo_r, whi_r, wlo_c, whi_c, pos, sub);
+        __syncthreads();   // counts final
+        pool_prefix<4>(s_vp);
+        __syncthreads();   // offsets final
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                {
-                    if (mask)
-                    {
-                        sel[q] = (int)__builtin_ctzll(mask);
-                        mask &= mask - 1;
-                    }
-                    else
-                    {
-                        sel[q] = -1;
-                    }
-                }
-                const int mine = kq == 0 ? sel[0] : kq == 1 ? sel[1] :
-                        kq == 2 ? sel[2] : sel[3];
-                float a = 0.0f, bre = 0.0f, bim = 0.0f;
-                if (mine >= 0)
-                {
+        for (int k = 0; k < 4; ++k)
+            if (sub[k] >= 0) s_pool[s_vp.offset[sub[k]] + pos[k]] = r;
+        __syncthreads();   // pool complete
+#pragma unroll
+        for (int cblk = 0; cblk < 4; ++cblk)
+        {
+            const int st = wave * 4 + cblk;
+            const int v_beg = __builtin_amdgcn_readfirstlane(
+                    (int)s_vp.offset[st]);
+            const int cnt = __builtin_amdgcn_readfirstlane((int)s_vp.count[st]);
+            const int my_v = tv0 + cblk * 16 + i;   // B col of this lane
+            const float fv = (float)my_v;
+            const float sgn_v = (my_v & 1) ? -1.0f : 1.0f;
+            for (int g = 0; g < cnt; g += 4)
+            {
 #pragma clang fp contract(off)
-                    const float4 r = s_rec[(bb + mine) * kVec];
-                    int u0, u1, v0, v1;
-                    tap_range(p, r.x, r.y, u0, u1, v0, v1);
-                    if (my_u >= u0 && my_u <= u1)
-                        a = sgn_u * es_tap(p.beta,
-                                ((float)my_u - r.x) * inv_hs);
-                    if (my_v >= v0 && my_v <= v1)
-                    {
-                        float kv = sgn_v * es_tap(p.beta,
-                                ((float)my_v - r.y) * inv_hs);
-                        if (DO_W) kv *= s_rec[(bb + mine) * kVec + 1].x;
-                        bre = kv * r.z;
-                        bim = kv * r.w;
-                    }
-                }
-                acc_re = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bre, acc_re,
-                        0, 0, 0);
-                acc_im = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bim, acc_im,
-                        0, 0, 0);
+                const int slot = g + kq;
+                const bool valid = slot < cnt;
+                const float4 q = s_pool[v_beg + (valid ? slot : cnt - 1)];
+                // Tap u lies in [ceil(pu - W/2), floor(pu + W/2)]
+                // (kernels.cu:332-335) iff pu - W/2 <= u <= pu + W/2.
+                const bool in_u = valid && q.x - hs <= fu && fu <= q.x + hs;
+                const bool in_v = valid && q.y - hs <= fv && fv <= q.y + hs;
+                const float ka = es_tap_fast(p.beta, (fu - q.x) * inv_hs);
+                const float kb = es_tap_fast(p.beta, (fv - q.y) * inv_hs);
+                const float a = in_u ? sgn_u * ka : 0.0f;
+                const float kv = in_v ? sgn_v * kb : 0.0f;
+                const float bre = kv * q.z, bim = kv * q.w;
+                acc_re[cblk] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bre,
+                        acc_re[cblk], 0, 0, 0);
+                acc_im[cblk] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bim,
+                        acc_im[cblk], 0, 0, 0);
             }
         }
     }
 
     // C/D layout of 16x16x4 f32: col = lane & 15, row = (lane >> 4)*4 + r.
-    const int col = c0 + sub_c + i;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int cblk = 0; cblk < 4; ++cblk)
     {
-        const int row = r0 + sub_r + kq * 4 + r;
-        if (row >= p.G || col >= p.G) continue;
-        float* dst = grid + ((size_t)row * p.G + col) * 2;
-        if (npieces == 1)
+        const int col = c0 + cblk * 16 + i;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
         {
-            float2 v;
-            v.x = acc_re[r];
-            v.y = acc_im[r];
-            *(float2*)dst = v;
+            const int row = r0 + sub_r + kq * 4 + r;
+            if (row >= p.G || col >= p.G) continue;
+            float* dst = grid + ((size_t)row * p.G + col) * 2;
+            if (npieces == 1)
+            {
+                float2 v;
+                v.x = acc_re[cblk][r];
+                v.y = acc_im[cblk][r];
+                *(float2*)dst = v;
+            }
+            else
+            {
+                if (acc_re[cblk][r] != 0.0f) unsafeAtomicAdd(dst, acc_re[cblk][r]);
+                if (acc_im[cblk][r] != 0.0f)
+                    unsafeAtomicAdd(dst + 1, acc_im[cblk][r]);
+            }
         }
-        else
+    }
+}
+
+// Degrid mode, f32, matrix-core form (the hot path).
+//
+// For visibility j and a 16x16 sub-tile (rows R, cols C) of the grid,
+//   partial_j = sum_r s_u ku_j[r] * (sum_c G[r][c] s_v kv_j[c])
+// The inner sums for 16 visibilities at once are T = G_sub * Kv, a
+// 16x16x16 product = four v_mfma_f32_16x16x4_f32 per re / im, with the
+// sub-tile's grid values as the A operand (loaded once per sub-tile from
+// the LDS window) and B[c][j] = the v-taps of visibility j. In the C
+// layout lane l holds T[4(l>>4)+r][l&15], so it applies four u-taps of
+// visibility l&15, and a two-step lane-group reduction gives partial_j.
+// Entries are bucketed by the tile of their first tap, so a tile's
+// entries reach into the next 16 rows / cols: the workgroup stages the
+// 80x80 window (tile + halo) in LDS and works on 5x5 sub-tiles; partials
+// of one visibility from several sub-tiles meet in an LDS accumulator
+// (16-lane ds_add_f32), and each visibility is read-modify-written in HBM
+// once.
+template<bool DO_W>
+__global__ __launch_bounds__(256) void k_gather_mfma(EsParams<float> p,
+        const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
+        const uint32_t* __restrict__ item_start,
+        const uint32_t* __restrict__ item_bin, const float* __restrict__ grid,
+        float* __restrict__ vis)
+{
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int kChunk = 256;
+    constexpr int kSub = 5;                 // 5 x 5 sub-tiles: tile + halo
+    __shared__ float4 s_pool[4 * kChunk];   // {pu, pv, kw*flip, e} per visit
+    __shared__ float s_acc_re[kChunk];
+    __shared__ float s_acc_im[kChunk];
+    __shared__ VisitPool<kSub> s_vp;
+
+    const uint32_t item = blockIdx.x;
+    const int b = (int)item_bin[item];
+    const uint32_t piece = item - item_start[b];
+    const uint32_t e0 = bin_start[b] + piece * kPiece;
+    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
+    if (e0 >= e1) return;   // empty tile
+    const int half = p.G / 2;
+    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    const int tu0 = r0 - half, tv0 = c0 - half;
+    const float2* g2 = (const float2*)grid;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int jl = lane & 15, kq = lane >> 4;
+    const float hs = (float)p.support / 2.0f;
+    const float inv_hs = 1.0f / hs;
+    const float4* recs4 = (const float4*)recs;
+
+    for (uint32_t cb = e0; cb < e1; cb += kChunk)
+    {
+        const int n = (int)min((uint32_t)kChunk, e1 - cb);
+        const int t = threadIdx.x;
+        __syncthreads();   // previous chunk consumed
+        if (t < kSub * kSub) s_vp.count[t] = 0;
+        float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        int wlo_r = 1, whi_r = 0, wlo_c = 1, whi_c = 0;
+        if (t < n)
         {
-            if (acc_re[r] != 0.0f) unsafeAtomicAdd(dst, acc_re[r]);
-            if (acc_im[r] != 0.0f) unsafeAtomicAdd(dst + 1, acc_im[r]);
+            r = recs4[cb + t];
+            int u0, u1, v0, v1;
+            tap_range(p, r.x, r.y, u0, u1, v0, v1);
+            wlo_r = (u0 - tu0) >> 4;
+            whi_r = min(u1 - tu0, kSub * 16 - 1) >> 4;
+            wlo_c = (v0 - tv0) >> 4;
+            whi_c = min(v1 - tv0, kSub * 16 - 1) >> 4;
+        }
+        s_acc_re[t] = 0.0f;
+        s_acc_im[t] = 0.0f;
+        __syncthreads();
+        int pos[4], sub[4];
+        pool_classify<kSub>(s_vp, lane, wlo_r, whi_r, wlo_c, whi_c, pos, sub);
+        __syncthreads();
+        pool_prefix<kSub>(s_vp);
+        __syncthreads();
+        const float4 q_mine = make_float4(r.x, r.y, r.z, __int_as_float(t));
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (sub[k] >= 0) s_pool[s_vp.offset[sub[k]] + pos[k]] = q_mine;
+        __syncthreads();
+        for (int st = wave; st < kSub * kSub; st += 4)
+        {
+            const int cnt = __builtin_amdgcn_readfirstlane((int)s_vp.count[st]);
+            if (cnt == 0) continue;
+            const int v_beg = __builtin_amdgcn_readfirstlane(
+                    (int)s_vp.offset[st]);
+            const int R0 = (st / kSub) * 16, C0 = (st % kSub) * 16;
+            // A operands straight from the grid (L2 / HBM):
+            // G[r0 + R0 + jl][c0 + C0 + 4 kk + kq], kk = 0..3.
+            float a_re[4], a_im[4];
+            const int grow = r0 + R0 + jl;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+            {
+                const int gcol = c0 + C0 + 4 * kk + kq;
+                float2 v = make_float2(0.0f, 0.0f);
+                if (grow < p.G && gcol < p.G) v = g2[(size_t)grow * p.G + gcol];
+                a_re[kk] = v.x;
+                a_im[kk] = v.y;
+            }
+            for (int g = 0; g < cnt; g += 16)
+            {
+#pragma clang fp contract(off)
+                const bool valid = g + jl < cnt;
+                const float4 q = s_pool[v_beg + (valid ? g + jl : cnt - 1)];
+                f32x4 t_re = {0.0f, 0.0f, 0.0f, 0.0f};
+                f32x4 t_im = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                {
+                    const int v = tv0 + C0 + 4 * kk + kq;
+                    const float fv = (float)v;
+                    const bool in_v = valid && q.y - hs <= fv && fv <= q.y + hs;
+                    const float k = es_tap_fast(p.beta, (fv - q.y) * inv_hs);
+                    const float kv = in_v ? ((v & 1) ? -k : k) : 0.0f;
+                    t_re = __builtin_amdgcn_mfma_f32_16x16x4f32(a_re[kk], kv,
+                            t_re, 0, 0, 0);
+                    t_im = __builtin_amdgcn_mfma_f32_16x16x4f32(a_im[kk], kv,
+                            t_im, 0, 0, 0);
+                }
+                float p_re = 0.0f, p_im = 0.0f;
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                {
+                    const int u = tu0 + R0 + 4 * kq + rr;
+                    const float fu = (float)u;
+                    const bool in_u = valid && q.x - hs <= fu && fu <= q.x + hs;
+                    const float k = es_tap_fast(p.beta, (fu - q.x) * inv_hs);
+                    const float ku = in_u ? ((u & 1) ? -k : k) : 0.0f;
+                    p_re += ku * t_re[rr];
+                    p_im += ku * t_im[rr];
+                }
+                // Sum the four lane groups (rows 4kq..4kq+3).
+                p_re += __shfl_xor(p_re, 16);
+                p_im += __shfl_xor(p_im, 16);
+                p_re += __shfl_xor(p_re, 32);
+                p_im += __shfl_xor(p_im, 32);
+                if (kq == 0 && valid)
+                {
+                    const int e = __float_as_int(q.w);
+                    const float kw = DO_W ? fabsf(q.z) : 1.0f;
+                    atomicAdd(&s_acc_re[e], p_re * kw);
+                    atomicAdd(&s_acc_im[e], p_im * kw);
+                }
+            }
+        }
+        __syncthreads();
+        if (t < n)
+        {
+            const uint64_t idx = (uint64_t)__float_as_uint(r.w);
+            const float flip = signbit(r.z) ? -1.0f : 1.0f;
+            vis[2 * idx] += s_acc_re[t];
+            vis[2 * idx + 1] += s_acc_im[t] * flip;   // kernels.cu:267-268
         }
     }
 }
@@ -720,14 +954,15 @@ __global__ __launch_bounds__(1024) void k_scatter_mfma(EsParams<float> p,
 template<typename T, bool DO_W>
 __global__ __launch_bounds__(kThreads) void k_gather(EsParams<T> p,
         const T* __restrict__ recs, const uint32_t* __restrict__ bin_start,
-        const uint32_t* __restrict__ item_start, const T* __restrict__ grid,
+        const uint32_t* __restrict__ item_start,
+        const uint32_t* __restrict__ item_bin, const T* __restrict__ grid,
         T* __restrict__ vis, int wrows, int ws)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     T* w_re = (T*)smem;
     T* w_im = w_re + wrows * ws;
     const uint32_t item = blockIdx.x;
-    const int b = find_bin(item_start, p.nbins, item);
+    const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
     const uint32_t e0 = bin_start[b] + piece * kPiece;
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
@@ -1031,7 +1266,7 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
             s->table, nc, p.nbins, s->bin_count);
     SDP_HIP_CHECK_LAUNCH(status);
     k_scan_bins<<<1, 1024, 0, stream>>>(s->bin_count, p.nbins, s->bin_start,
-            s->item_start, s->totals);
+            s->item_start, s->totals, s->item_bin, s->item_capacity);
     SDP_HIP_CHECK_LAUNCH(status);
     SDP_HIP_CHECK(hipMemcpyAsync(s->totals_host, s->totals,
             2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream), status);
@@ -1084,11 +1319,11 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     if constexpr (sizeof(T) == 4)
     {
         if (p.do_w)
-            k_scatter_mfma<true><<<n_items, 1024, 0, stream>>>(
-                    p, (const float*)s.recs, s.bin_start, s.item_start, grid);
+            k_scatter_mfma<true><<<n_items, 256, 0, stream>>>(
+                    p, (const float*)s.recs, s.bin_start, s.item_start, s.item_bin, grid);
         else
-            k_scatter_mfma<false><<<n_items, 1024, 0, stream>>>(
-                    p, (const float*)s.recs, s.bin_start, s.item_start, grid);
+            k_scatter_mfma<false><<<n_items, 256, 0, stream>>>(
+                    p, (const float*)s.recs, s.bin_start, s.item_start, s.item_bin, grid);
         SDP_HIP_CHECK_LAUNCH(status);
         return *status;
     }
@@ -1097,13 +1332,13 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     {
         SDP_HIP_CHECK(((hipError_t)allow_lds<k_scatter<T, true>>(lds)), status);
         k_scatter<T, true><<<n_items, kThreads, lds, stream>>>(
-                p, (const T*)s.recs, s.bin_start, s.item_start, grid);
+                p, (const T*)s.recs, s.bin_start, s.item_start, s.item_bin, grid);
     }
     else
     {
         SDP_HIP_CHECK(((hipError_t)allow_lds<k_scatter<T, false>>(lds)), status);
         k_scatter<T, false><<<n_items, kThreads, lds, stream>>>(
-                p, (const T*)s.recs, s.bin_start, s.item_start, grid);
+                p, (const T*)s.recs, s.bin_start, s.item_start, s.item_bin, grid);
     }
     SDP_HIP_CHECK_LAUNCH(status);
     return *status;
@@ -1115,6 +1350,22 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
 {
     sdp_Error st = SDP_SUCCESS;
     sdp_Error* status = &st;
+    if constexpr (sizeof(T) == 4)
+    {
+        if (p.support <= 16)
+        {
+            if (p.do_w)
+                k_gather_mfma<true><<<n_items, 256, 0, stream>>>(
+                        p, (const float*)s.recs, s.bin_start, s.item_start,
+                        s.item_bin, grid, vis);
+            else
+                k_gather_mfma<false><<<n_items, 256, 0, stream>>>(
+                        p, (const float*)s.recs, s.bin_start, s.item_start,
+                        s.item_bin, grid, vis);
+            SDP_HIP_CHECK_LAUNCH(status);
+            return *status;
+        }
+    }
     const int wrows = kTile + p.support;
     int ws = wrows;
     while (ws % 32 != 8 && ws % 32 != 24) ++ws;
@@ -1128,15 +1379,15 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     {
         SDP_HIP_CHECK(((hipError_t)allow_lds<k_gather<T, true>>(lds)), status);
         k_gather<T, true><<<n_items, kThreads, lds, stream>>>(p,
-                (const T*)s.recs, s.bin_start, s.item_start, grid, vis, wrows,
-                ws);
+                (const T*)s.recs, s.bin_start, s.item_start, s.item_bin, grid,
+                vis, wrows, ws);
     }
     else
     {
         SDP_HIP_CHECK(((hipError_t)allow_lds<k_gather<T, false>>(lds)), status);
         k_gather<T, false><<<n_items, kThreads, lds, stream>>>(p,
-                (const T*)s.recs, s.bin_start, s.item_start, grid, vis, wrows,
-                ws);
+                (const T*)s.recs, s.bin_start, s.item_start, s.item_bin, grid,
+                vis, wrows, ws);
     }
     SDP_HIP_CHECK_LAUNCH(status);
     return *status;

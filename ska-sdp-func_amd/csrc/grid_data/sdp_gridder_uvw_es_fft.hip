@@ -188,6 +188,18 @@ void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
 {
     if (*status) return;
     sdp_es::BucketScratch& s = plan->scratch;
+    // Work items: at least one per bin, plus one per kPiece entries (a
+    // visibility is listed in at most 4 tiles).
+    const size_t items = 2 * (size_t)plan->nbins + 1 +
+            (size_t)(4 * num_vis) / sdp_es::kPiece;
+    if (items > s.item_capacity)
+    {
+        if (s.item_bin) SDP_HIP_CHECK(hipFree(s.item_bin), status);
+        s.item_bin = nullptr;
+        SDP_HIP_CHECK(hipMalloc(&s.item_bin, items * sizeof(uint32_t)),
+                status);
+        s.item_capacity = *status ? 0 : (uint32_t)items;
+    }
     const size_t need = (size_t)sdp_es::num_chunks(num_vis) * plan->nbins;
     if (need > s.table_entries)
     {
@@ -370,6 +382,7 @@ void sdp_gridder_uvw_es_fft_free_plan(sdp_GridderUvwEsFft* plan)
     if (plan->tables) (void)hipFree(plan->tables);
     sdp_es::BucketScratch& s = plan->scratch;
     if (s.table) (void)hipFree(s.table);
+    if (s.item_bin) (void)hipFree(s.item_bin);
     if (s.bin_count) (void)hipFree(s.bin_count);
     if (s.recs) (void)hipFree(s.recs);
     if (s.totals_host) (void)hipHostFree(s.totals_host);
