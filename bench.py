@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--eps", type=float, default=1e-5)
     ap.add_argument("--reduce", choices=["image", "grid"], default="image")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-rows", type=int, default=2_000_000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=10_000_000)
     ap.add_argument("--no-degrid", action="store_true")
     return ap.parse_args()
 
@@ -96,13 +96,15 @@ def gridding_bytes(rows, chan, G, n):
 
 
 def cpu_baseline(args, G, support, beta, uv_scale):
-    """Oracle ('port') gridder on the host cores, bounded sample.
+    """Oracle ('port') CPU gridder timed on the host cores.
 
-    The f32 OpenMP scatter of oracle/es_oracle.c is timed on
-    --cpu-sample-rows rows of the same synthetic distribution, the fixed
-    costs (per-thread grid reduce, included in that call; 8192^2 FFT with
-    scipy pocketfft on all threads; screen + correction) are timed once, and
-    the rate for the full job is extrapolated linearly in rows.
+    The whole config-2 gridding call on the CPU: the stripe-binned OpenMP
+    f32 scatter of oracle/es_oracle.c (same taps as the reference), a
+    multi-threaded pocketfft (scipy) inverse FFT of the grid, and the crop +
+    checkerboard + correction of the image in numpy. Run on the same number
+    of rows as the GPU step when --cpu-sample-rows >= --rows, else on that
+    many rows with the scatter time scaled linearly (the FFT and image steps
+    do not depend on the row count).
     """
     import scipy.fft
 
@@ -110,15 +112,15 @@ def cpu_baseline(args, G, support, beta, uv_scale):
 
     lib = es_oracle.lib()
     threads = min(16, os.cpu_count() or 1)
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    n_s = min(args.cpu_sample_rows, args.rows)
     rng = np.random.default_rng(20251015 + 2)
-    n_s = args.cpu_sample_rows
     px = 2.0 * np.pi / 180.0 / args.image
     umax = 0.45 * C_LIGHT / (1e9 * px)
     r = umax * np.sqrt(rng.random(n_s))
     th = 2 * np.pi * rng.random(n_s)
     uvw = np.stack([r * np.cos(th), r * np.sin(th),
                     rng.uniform(-500, 500, n_s)], 1).astype(np.float32)
+    del r, th
     vis = (rng.standard_normal((n_s, 1)) + 1j * rng.standard_normal(
         (n_s, 1))).astype(np.complex64)
     wt = np.ones((n_s, 1), np.float32)
@@ -132,36 +134,30 @@ def cpu_baseline(args, G, support, beta, uv_scale):
                                       float(np.float32(uv_scale)),
                                       es_oracle._ptr(grid))
     t_scatter = time.perf_counter() - t0
-    # Fixed part of the scatter call (per-thread grid zero + reduce):
-    t0 = time.perf_counter()
-    lib.oracle_es_grid_f32_omp(0, 1, es_oracle._ptr(uvw),
-                               es_oracle._ptr(freq), es_oracle._ptr(vis),
-                               es_oracle._ptr(wt), G, support,
-                               float(np.float32(beta)),
-                               float(np.float32(uv_scale)),
-                               es_oracle._ptr(grid))
-    t_fixed_scatter = time.perf_counter() - t0
     t0 = time.perf_counter()
     layer = scipy.fft.ifft2(grid, norm="forward", workers=threads,
                             overwrite_x=True)
     h, gc = args.image // 2, G // 2
-    sub = layer[gc - h:gc + h, gc - h:gc + h].real
-    img = sub * np.float32(1.0001)   # stands in for screen + correction
+    off = np.arange(-h, h)
+    sgn = np.where(((off[:, None] + off[None, :]) & 1) != 0, -1.0, 1.0)
+    img = (layer[gc - h:gc + h, gc - h:gc + h].real * sgn).astype(np.float32)
+    img *= np.float32(1.0001)   # separable correction multiply
     t_fft_img = time.perf_counter() - t0
-    del layer, img
-    per_row = max(t_scatter - t_fixed_scatter, 1e-9) / n_s
-    t_job = per_row * args.rows * args.chan + t_fixed_scatter + t_fft_img
+    del layer, img, grid
+    scale = args.rows * args.chan / n_s
+    t_job = t_scatter * scale + t_fft_img
     return {
         "value": args.rows * args.chan / t_job / 1e6,
         "unit": "Mvis/s",
         "cores": int(used),
         "kind": "port",
-        "sample": (f"oracle/es_oracle.c f32 OpenMP scatter on {n_s} rows of "
-                   f"the config-2 distribution ({t_scatter:.2f} s incl. "
-                   f"{t_fixed_scatter:.2f} s per-thread grid zero+reduce), "
-                   f"scipy pocketfft ifft2 {G}^2 c64 + crop "
-                   f"({t_fft_img:.2f} s), extrapolated linearly to "
-                   f"{args.rows} rows"),
+        "sample": (f"oracle/es_oracle.c stripe-binned OpenMP f32 scatter of "
+                   f"{n_s} config-2 rows ({t_scatter:.3f} s"
+                   + (f", x{scale:.2f} to {args.rows} rows" if scale != 1
+                      else "")
+                   + f") + scipy pocketfft ifft2 {G}^2 c64 on {threads} "
+                   f"threads + crop/checkerboard/correction "
+                   f"({t_fft_img:.3f} s)"),
     }
 
 
@@ -194,19 +190,16 @@ def main():
     if world > 1 and args.reduce == "grid":
         grid_buf = torch.empty((G, G), dtype=torch.complex64, device=dev)
 
+    from ska_sdp_func.grid_data.distributed import grid_sharded
+
     def grid_step():
         # Fresh image per step (the call accumulates into it).
         dirty.zero_()
         if world == 1:
             plan.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
-        elif args.reduce == "image":
-            plan.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
-            dist.reduce(dirty, dst=0)
         else:
-            plan.grid_scatter(uvw, freq, vis, weight, grid_buf)
-            dist.reduce(grid_buf, dst=0)
-            if rank == 0:
-                plan.grid_finish(grid_buf, dirty)
+            grid_sharded(plan, uvw, freq, vis, weight, dirty, dist,
+                         mode=args.reduce, dst=0, grid_buf=grid_buf)
 
     def barrier():
         torch.cuda.synchronize(dev)

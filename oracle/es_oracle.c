@@ -274,10 +274,13 @@ void oracle_es_degrid_f64(
 }
 
 /*
- * CPU baseline leg (bench.py only): the same f32 scatter, parallelised over
- * rows with one private f32 grid per thread and a final reduction; this is a
- * straightforward OpenMP CPU gridder of the reference's arithmetic. Returns
- * the number of threads used.
+ * CPU baseline leg (bench.py only): a multi-threaded CPU gridder of the
+ * reference's f32 arithmetic (same taps as visit_f32). Grid rows are split
+ * into stripes; visibilities are binned by the stripes their taps touch
+ * (counting sort, per-thread counts), then threads take whole stripes, so
+ * every grid cell is written by one thread: no private grids, no atomics.
+ * Accumulates into grid_out (complex64, interleaved). Returns the number of
+ * OpenMP threads used.
  */
 int oracle_es_grid_f32_omp(
         int64_t num_rows, int num_chan, const float* uvw, const float* freq,
@@ -288,65 +291,125 @@ int oracle_es_grid_f32_omp(
 #ifdef _OPENMP
     nthreads = omp_get_max_threads();
 #endif
-    const size_t cells = (size_t)G * G;
-    float* priv = (float*)calloc((size_t)nthreads * cells * 2, sizeof(float));
-    if (!priv) return -1;
+    const int64_t nvis = num_rows * num_chan;
+    const int nstripes = 8 * nthreads;
+    const int rows_per = (G + nstripes - 1) / nstripes;
+    const float half_support = (float)support / 2.0f;
+    const float inv_hs = 1.0f / half_support;
+    const int off = G / 2;
+    int64_t* counts = (int64_t*)calloc((size_t)nthreads * (nstripes + 1),
+            sizeof(int64_t));
+    if (!counts) return -1;
+    /* pass 1: count (vis, stripe) entries per thread */
 #pragma omp parallel
     {
         int tid = 0;
 #ifdef _OPENMP
         tid = omp_get_thread_num();
 #endif
-        float* g = priv + (size_t)tid * cells * 2;
-        const float half_support = (float)support / 2.0f;
-        const float inv_hs = 1.0f / half_support;
-        const int off = G / 2;
+        int64_t* my = counts + (size_t)tid * (nstripes + 1);
 #pragma omp for schedule(static)
-        for (int64_t r = 0; r < num_rows; ++r)
+        for (int64_t i = 0; i < nvis; ++i)
         {
-            for (int c = 0; c < num_chan; ++c)
+            const int64_t r = i / num_chan;
+            const int c = (int)(i - r * num_chan);
+            const float inv_wl = 1.0f * freq[c] / (float)C_LIGHT;
+            const float pu = uvw[3 * r] * inv_wl * uv_scale;
+            int u0 = (int)ceilf(pu - half_support);
+            int u1 = (int)floorf(pu + half_support);
+            if (u0 < -off) u0 = -off;
+            if (u1 > (G - 1) / 2) u1 = (G - 1) / 2;
+            if (u0 > u1) continue;
+            for (int s = (u0 + off) / rows_per; s <= (u1 + off) / rows_per; ++s)
+                my[s]++;
+        }
+    }
+    /* prefix: stripe-major, thread-minor */
+    int64_t* start = (int64_t*)calloc((size_t)nstripes + 1, sizeof(int64_t));
+    int64_t total = 0;
+    for (int s = 0; s < nstripes; ++s)
+    {
+        start[s] = total;
+        for (int t = 0; t < nthreads; ++t)
+        {
+            const int64_t n = counts[(size_t)t * (nstripes + 1) + s];
+            counts[(size_t)t * (nstripes + 1) + s] = total;
+            total += n;
+        }
+    }
+    start[nstripes] = total;
+    int64_t* list = (int64_t*)malloc((size_t)(total > 0 ? total : 1) *
+            sizeof(int64_t));
+    /* pass 2: fill (same static schedule -> same thread/chunk mapping) */
+#pragma omp parallel
+    {
+        int tid = 0;
+#ifdef _OPENMP
+        tid = omp_get_thread_num();
+#endif
+        int64_t* my = counts + (size_t)tid * (nstripes + 1);
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < nvis; ++i)
+        {
+            const int64_t r = i / num_chan;
+            const int c = (int)(i - r * num_chan);
+            const float inv_wl = 1.0f * freq[c] / (float)C_LIGHT;
+            const float pu = uvw[3 * r] * inv_wl * uv_scale;
+            int u0 = (int)ceilf(pu - half_support);
+            int u1 = (int)floorf(pu + half_support);
+            if (u0 < -off) u0 = -off;
+            if (u1 > (G - 1) / 2) u1 = (G - 1) / 2;
+            if (u0 > u1) continue;
+            for (int s = (u0 + off) / rows_per; s <= (u1 + off) / rows_per; ++s)
+                list[my[s]++] = i;
+        }
+    }
+    /* pass 3: each stripe by one thread */
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int s = 0; s < nstripes; ++s)
+    {
+        const int row_lo = s * rows_per - off;
+        const int row_hi = row_lo + rows_per - 1;
+        for (int64_t e = start[s]; e < start[s + 1]; ++e)
+        {
+            const int64_t i = list[e];
+            const int64_t r = i / num_chan;
+            const int c = (int)(i - r * num_chan);
+            const float inv_wl = 1.0f * freq[c] / (float)C_LIGHT;
+            const float pu = uvw[3 * r] * inv_wl * uv_scale;
+            const float pv = uvw[3 * r + 1] * inv_wl * uv_scale;
+            int u0 = (int)ceilf(pu - half_support);
+            int u1 = (int)floorf(pu + half_support);
+            int v0 = (int)ceilf(pv - half_support);
+            int v1 = (int)floorf(pv + half_support);
+            if (u0 < -off) u0 = -off;
+            if (v0 < -off) v0 = -off;
+            if (u1 > (G - 1) / 2) u1 = (G - 1) / 2;
+            if (v1 > (G - 1) / 2) v1 = (G - 1) / 2;
+            if (v0 > v1) continue;
+            const int a0 = u0 > row_lo ? u0 : row_lo;
+            const int a1 = u1 < row_hi ? u1 : row_hi;
+            float kv[64];
+            for (int v = v0; v <= v1; ++v)
+                kv[v - v0] = es_f(beta, ((float)v - pv) * inv_hs);
+            const float vre = vis[2 * i] * weight[i];
+            const float vim = vis[2 * i + 1] * weight[i];
+            for (int u = a0; u <= a1; ++u)
             {
-                const int64_t i = r * num_chan + c;
-                const float inv_wl = 1.0f * freq[c] / (float)C_LIGHT;
-                const float pu = uvw[3 * r] * inv_wl * uv_scale;
-                const float pv = uvw[3 * r + 1] * inv_wl * uv_scale;
-                int u0 = (int)ceilf(pu - half_support);
-                int u1 = (int)floorf(pu + half_support);
-                int v0 = (int)ceilf(pv - half_support);
-                int v1 = (int)floorf(pv + half_support);
-                if (u0 < -off) u0 = -off;
-                if (v0 < -off) v0 = -off;
-                if (u1 > (G - 1) / 2) u1 = (G - 1) / 2;
-                if (v1 > (G - 1) / 2) v1 = (G - 1) / 2;
-                if (u0 > u1 || v0 > v1) continue;
-                float ku[64], kv[64];
-                for (int u = u0; u <= u1; ++u)
-                    ku[u - u0] = es_f(beta, ((float)u - pu) * inv_hs);
+                const float ku = es_f(beta, ((float)u - pu) * inv_hs);
+                float* row = grid_out + 2 * ((size_t)(u + off) * G + off);
                 for (int v = v0; v <= v1; ++v)
-                    kv[v - v0] = es_f(beta, ((float)v - pv) * inv_hs);
-                const float vre = vis[2 * i] * weight[i];
-                const float vim = vis[2 * i + 1] * weight[i];
-                for (int u = u0; u <= u1; ++u)
                 {
-                    float* row = g + 2 * ((size_t)(u + off) * G + off);
-                    for (int v = v0; v <= v1; ++v)
-                    {
-                        float k = ku[u - u0] * kv[v - v0];
-                        if ((u + v) & 1) k = -k;
-                        row[2 * v] += vre * k;
-                        row[2 * v + 1] += vim * k;
-                    }
+                    float k = ku * kv[v - v0];
+                    if ((u + v) & 1) k = -k;
+                    row[2 * v] += vre * k;
+                    row[2 * v + 1] += vim * k;
                 }
             }
         }
-#pragma omp for schedule(static)
-        for (int64_t j = 0; j < (int64_t)(2 * cells); ++j)
-        {
-            float s = 0.0f;
-            for (int t = 0; t < nthreads; ++t) s += priv[(size_t)t * cells * 2 + j];
-            grid_out[j] += s;
-        }
     }
-    free(priv);
+    free(list);
+    free(start);
+    free(counts);
     return nthreads;
 }

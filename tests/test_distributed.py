@@ -1,0 +1,115 @@
+"""Multi-process (world_size 2, gloo, CPU) tests of the row-sharded gridding
+layer ska_sdp_func/grid_data/distributed.py -- the code bench.py runs over
+RCCL on GPUs. The per-rank gridder here is the CPU oracle behind the same
+duck-typed interface, so the decomposition (row shards, image reduce,
+grid reduce + single finish, input image only on the destination) is
+checked against the un-sharded oracle result.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from es_data import make_case, rel_l2
+
+
+class OracleGridder:
+    """CPU stand-in with the GridderUvwEsFft interface (oracle maths)."""
+
+    def __init__(self, geo):
+        self.geo = geo
+        self.grid_size = geo["grid_size"]
+
+    def grid_uvw_es_fft(self, uvw, freq, vis, weight, dirty):
+        from oracle import es_oracle
+
+        out = es_oracle.grid_uvw_es_fft(self.geo, uvw.numpy(), freq.numpy(),
+                                        vis.numpy(), weight.numpy(),
+                                        dirty.numpy())
+        dirty.copy_(torch.from_numpy(out))
+
+    def grid_scatter(self, uvw, freq, vis, weight, grid):
+        from oracle import es_oracle
+
+        g = es_oracle.scatter(self.geo, uvw.numpy(), freq.numpy(),
+                              vis.numpy(), weight.numpy())
+        grid.copy_(torch.from_numpy(g))
+
+    def grid_finish(self, grid, dirty):
+        from oracle import es_oracle
+
+        n = self.geo["image_size"]
+        G = self.grid_size
+        half, gc = n // 2, G // 2
+        layer = np.fft.ifft2(grid.numpy(), norm="forward")
+        off = np.arange(-half, half)
+        sgn = np.where(((off[:, None] + off[None, :]) & 1) != 0, -1.0, 1.0)
+        d = dirty.numpy().astype(np.float64)
+        d[:2 * half, :2 * half] += sgn * layer[gc - half:gc + half,
+                                               gc - half:gc + half].real
+        d[:2 * half, :2 * half] *= es_oracle.correction_map(self.geo)
+        dirty.copy_(torch.from_numpy(d))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, mode, result_path):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    for p in (here, root, os.path.join(root, "ska-sdp-func_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle import es_oracle
+    from ska_sdp_func.grid_data.distributed import grid_sharded, shard_rows
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 64
+    uvw, freq, vis, wt, px = make_case(31, 301, 2, n, dbl=True)
+    dirty_in = np.random.default_rng(5).standard_normal((n, n))
+    geo = es_oracle.geometry_for(uvw, freq, vis, dirty_in, px, 1e-10, False)
+    lo, hi = shard_rows(len(uvw), rank, world)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    dirty = t(dirty_in.copy())
+    G = geo["grid_size"]
+    grid_buf = torch.zeros((G, G), dtype=torch.complex128)
+    grid_sharded(OracleGridder(geo), t(uvw[lo:hi]), t(freq), t(vis[lo:hi]),
+                 t(wt[lo:hi]), dirty, dist, mode=mode, dst=0,
+                 grid_buf=grid_buf)
+    if rank == 0:
+        ref = es_oracle.grid_uvw_es_fft(geo, uvw, freq, vis, wt, dirty_in)
+        np.save(result_path, np.array([rel_l2(dirty.numpy(), ref)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["image", "grid"])
+def test_sharded_gridding_matches_unsharded(tmp_path, mode):
+    path = str(tmp_path / "err.npy")
+    mp.spawn(_worker, args=(2, _free_port(), mode, path), nprocs=2,
+             join=True)
+    err = float(np.load(path)[0])
+    assert err < 1e-12
+
+
+def test_shard_rows_cover_exactly():
+    from ska_sdp_func.grid_data.distributed import shard_rows
+
+    for n in (0, 1, 7, 10, 1001):
+        for w in (1, 2, 3, 8):
+            spans = [shard_rows(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for a, b in zip(spans, spans[1:]):
+                assert a[1] == b[0]
+            assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
