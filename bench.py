@@ -270,7 +270,7 @@ def main():
     dom = max(avg, key=lambda k: avg[k]) if any(avg.values()) else "tile_kernel"
     achieved = (kern_bytes[dom] / (avg[dom] * 1e-3) / 1e9
                 if avg.get(dom) else None)
-    kernel_names = {"tile_kernel": "k_scatter (LDS tile accumulation)",
+    kernel_names = {"tile_kernel": "k_scatter_mfma (MFMA tile accumulation)",
                     "fft": "rocFFT 2-D C2C inverse",
                     "bucket": "bucketing (count/scan/fill)",
                     "image": "k_screen_corr_2d"}
