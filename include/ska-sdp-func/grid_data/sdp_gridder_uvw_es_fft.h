@@ -85,6 +85,11 @@ int sdp_gridder_uvw_es_fft_support(const sdp_GridderUvwEsFft* plan);
 int sdp_gridder_uvw_es_fft_num_w_planes(const sdp_GridderUvwEsFft* plan);
 double sdp_gridder_uvw_es_fft_beta(const sdp_GridderUvwEsFft* plan);
 
+/* 1 if the plan uses the pruned, fused FFT passes (f32, power-of-two grid
+ * of 1024..16384 cells; environment SDP_ES_FFT=rocfft at plan creation
+ * selects rocFFT + separate screen kernels instead), 0 for rocFFT. */
+int sdp_gridder_uvw_es_fft_fused_fft(const sdp_GridderUvwEsFft* plan);
+
 /* Run the plan's work on a caller-owned hipStream_t (NULL = null stream). */
 void sdp_gridder_uvw_es_fft_set_stream(sdp_GridderUvwEsFft* plan,
         void* hip_stream);

@@ -1,0 +1,68 @@
+// Pruned, fused 2-D FFT between the uv grid and the image crop (f32).
+//
+// Replaces, for power-of-two grids, the full G x G cuFFT/rocFFT transform
+// plus the separate screen/correction kernels of the reference
+// (sdp_gridder_uvw_es_fft.cpp:660-740 gridding, :781-890 degridding).
+// Only the central M x M block of the transformed grid is ever used
+// (M = 2 * (N / 2)), so the transform is done in three HBM passes, all in
+// place in the grid buffer, with the image-plane work fused into the pass
+// that touches the image:
+//
+//  gridding (inverse, +i):
+//   rows   : length-G FFT of every grid row in LDS; keeps the M centre
+//            outputs (row u of the buffer now holds H[u][0..M)).
+//   col-A  : four-step, G = N1 * N2: length-N2 FFTs down the rows
+//            u1 + N1 * n2 of each column, times W_G^(u1 k2), in place.
+//   col-B  : length-N1 FFTs over the contiguous row block N1 * k2 + n1;
+//            output row k = k2 + N2 * k1 of the centre goes straight into
+//            the image with the screen + correction epilogue
+//            (2-D: dirty = (dirty + checker * Re) / correction;
+//             3-D: dirty += checker * Re(F * phasor(w)), per plane).
+//  degridding (forward, -i): the mirror image -- the first column pass reads
+//   the (corrected in place) image with the checker / phasor prologue, the
+//   row pass zero-pads and writes every cell of the grid.
+//
+// HBM traffic per call at G = 8192, N = 5440: ~2.2 GB (rocFFT + separate
+// screen: ~4.8 GB). Twiddles are read once per workgroup from a G-entry
+// table computed in double on the host and kept in registers; in-register
+// DFTs use compile-time roots of unity.
+#ifndef SDP_ES_FFT_H_
+#define SDP_ES_FFT_H_
+
+#include <hip/hip_runtime.h>
+
+#include "es_kernels.h"
+
+namespace sdp_es {
+
+// Grids the fused path handles: G a power of two in [1024, 16384].
+bool fused_fft_supported(int grid_size);
+
+// Twiddle table exp(-2 pi i m / G), m in [0, G), as float2 in device memory.
+struct FftTwiddles
+{
+    void* table = nullptr;
+    int G = 0;
+};
+int fft_twiddles_create(int grid_size, FftTwiddles* tw);
+void fft_twiddles_destroy(FftTwiddles* tw);
+
+// Gridding, part 1: row pass + first column pass (in place on grid).
+int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
+        float* grid, hipStream_t stream);
+// Gridding, part 2: last column pass + screen/correction into dirty.
+int fft_grid_to_image(const ImageParams<float>& ip, int plane,
+        const FftTwiddles& tw, float* grid, float* dirty, hipStream_t stream);
+
+// Degridding, part 1: image prologue (2-D: correct dirty in place) + first
+// column pass into the grid buffer.
+int fft_image_cols(const ImageParams<float>& ip, int plane,
+        const FftTwiddles& tw, float* dirty, bool correct_in_place,
+        float* grid, hipStream_t stream);
+// Degridding, part 2: second column pass + row pass writing every grid cell.
+int fft_image_to_grid(const ImageParams<float>& ip, const FftTwiddles& tw,
+        float* grid, hipStream_t stream);
+
+} // namespace sdp_es
+
+#endif

@@ -9,13 +9,16 @@
 
 #include "es_kernels.h"
 #include "es_params.h"
+#include "es_image_dev.h"
 #include "../utility/sdp_hip.h"
 
 namespace sdp_es {
 namespace {
 
+using img::inv_correction;
+using img::phasor;
+
 constexpr double kSpeedOfLight = 299792458.0;
-constexpr double kPi = 3.1415926535897931;
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kScatterStride = kTile + 8;   // 72 = 8 (mod 32): conflict-free
@@ -1070,71 +1073,6 @@ __global__ __launch_bounds__(kThreads) void k_gather(EsParams<T> p,
 
 // Image-plane kernels ---------------------------------------------------------
 
-// conv_corr device function, kernels.cu:69-87 (cos argument in double as the
-// reference's double PI literal promotes it).
-template<typename T>
-__device__ T conv_corr_n(const ImageParams<T>& ip, T k)
-{
-    const T support = (T)ip.support;
-    const uint32_t np = (uint32_t)ceil(T(1.5) * support + T(2));
-    T c = T(0);
-    for (uint32_t i = 0; i < np; ++i)
-    {
-        c = (T)((double)c + (double)ip.quad_kernel[i] *
-                cos(kPi * (double)k * (double)support *
-                (double)ip.quad_nodes[i]) * (double)ip.quad_weights[i]);
-    }
-    return c * support;
-}
-
-// 1 / correction at pixel offsets (i = |x| column, j = |y| row),
-// kernels.cu:711-740.
-template<typename T>
-__device__ T inv_correction(const ImageParams<T>& ip, int i, int j)
-{
-#pragma clang fp contract(off)
-    const T l_conv = ip.conv_corr[i], m_conv = ip.conv_corr[j];
-    T corr;
-    if (ip.do_w)
-    {
-        const T l = ip.pixel_size * (T)i, m = ip.pixel_size * (T)j;
-        const T n = sqrt(T(1) - l * l - m * m) - T(1);
-        T n_conv = conv_corr_n(ip, n * ip.inv_w_scale);
-        n_conv *= (ip.norm * ip.norm);
-        corr = l_conv * m_conv * n_conv;
-    }
-    else
-    {
-        corr = l_conv * m_conv * ip.norm * ip.norm;
-    }
-    return T(1) / corr;
-}
-
-__device__ __forceinline__ void sin_cos(float x, float* s, float* c)
-{
-    sincosf(x, s, c);
-}
-__device__ __forceinline__ void sin_cos(double x, double* s, double* c)
-{
-    sincos(x, s, c);
-}
-
-// w-screen phasor, kernels.cu:110-123.
-template<typename T>
-__device__ void phasor(const ImageParams<T>& ip, int plane, int i, int j,
-        T sign, T& re, T& im)
-{
-#pragma clang fp contract(off)
-    const T l = ip.pixel_size * (T)i, m = ip.pixel_size * (T)j;
-    const T w = (T)plane * ip.inv_w_scale + ip.min_plane_w;
-    const T sos = l * l + m * m;
-    const T nm1 = (-sos) / (sqrt(T(1) - sos) + T(1));
-    const T x = T(2) * T(kPi) * w * nm1;
-    const T xn = T(1) / (nm1 + T(1));
-    sin_cos(sign * x, &im, &re);
-    re *= xn;
-    im *= xn;
-}
 
 template<typename T>
 __global__ void k_screen_corr_2d(ImageParams<T> ip, const T* __restrict__ layer,

@@ -11,11 +11,13 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "ska-sdp-func/grid_data/sdp_gridder_uvw_es_fft.h"
 #include "es_kernels.h"
 #include "es_params.h"
 #include "../fft/fft2d.h"
+#include "es_fft.h"
 #include "../utility/sdp_hip.h"
 
 struct sdp_GridderUvwEsFft
@@ -49,7 +51,9 @@ struct sdp_GridderUvwEsFft
     int ntiles;
     int nbins;
     sdp_es::BucketScratch scratch;
-    sdp_fft::Plan2D* fft;
+    sdp_fft::Plan2D* fft;       // rocFFT (f64, or grids es_fft does not take)
+    int fused_fft;              // f32 power-of-two grid: pruned fused passes
+    sdp_es::FftTwiddles fft_tw;
     hipStream_t stream;
 
     // Timing.
@@ -289,6 +293,68 @@ void scatter_plane(sdp_GridderUvwEsFft* plan, int plane, int64_t rows,
     timing_mark(plan, 2);
 }
 
+// FFT of the gridded plane + image-plane step into dirty (per plane): the
+// fused pruned passes (f32, es_fft.h) or rocFFT + screen kernels.
+template<typename T>
+void grid_to_image(sdp_GridderUvwEsFft* plan,
+        const sdp_es::ImageParams<T>& ip, int plane, T* grid, T* dirty,
+        sdp_Error* status)
+{
+    if (*status) return;
+    int e = 0;
+    if constexpr (std::is_same<T, float>::value)
+    {
+        if (plan->fused_fft)
+        {
+            e = sdp_es::fft_grid_rows_cols(ip, plan->fft_tw, grid,
+                    plan->stream);
+            if (e) { *status = (sdp_Error)e; return; }
+            timing_mark(plan, 3);
+            e = sdp_es::fft_grid_to_image(ip, plane, plan->fft_tw, grid,
+                    dirty, plan->stream);
+            if (e) *status = (sdp_Error)e;
+            return;
+        }
+    }
+    sdp_fft::exec_2d(plan->fft, grid, false, plan->stream, status);
+    timing_mark(plan, 3);
+    if (*status) return;
+    e = plan->do_wstacking ?
+            sdp_es::screen_accumulate<T>(ip, plane, grid, dirty,
+                    plan->stream) :
+            sdp_es::screen_corr_2d<T>(ip, grid, dirty, plan->stream);
+    if (e) *status = (sdp_Error)e;
+}
+
+// Degridding: image (2-D: corrected in place) -> this plane's grid.
+template<typename T>
+void image_to_grid(sdp_GridderUvwEsFft* plan,
+        const sdp_es::ImageParams<T>& ip, int plane, T* dirty, T* grid,
+        sdp_Error* status)
+{
+    if (*status) return;
+    int e = 0;
+    if constexpr (std::is_same<T, float>::value)
+    {
+        if (plan->fused_fft)
+        {
+            e = sdp_es::fft_image_cols(ip, plane, plan->fft_tw, dirty,
+                    !plan->do_wstacking, grid, plan->stream);
+            if (e) { *status = (sdp_Error)e; return; }
+            timing_mark(plan, 2);
+            e = sdp_es::fft_image_to_grid(ip, plan->fft_tw, grid,
+                    plan->stream);
+            if (e) *status = (sdp_Error)e;
+            return;
+        }
+    }
+    e = sdp_es::reverse_screen<T>(ip, plane, dirty, !plan->do_wstacking,
+            grid, plan->stream);
+    if (e) { *status = (sdp_Error)e; return; }
+    timing_mark(plan, 2);
+    sdp_fft::exec_2d(plan->fft, grid, true, plan->stream, status);
+}
+
 template<typename T>
 void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
         const T* uvw, const T* freq, const T* vis, const T* weight, T* dirty,
@@ -301,19 +367,13 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
     {
         scatter_plane<T>(plan, plane, rows, chan, uvw, freq, vis, weight,
                 grid, status);
-        sdp_fft::exec_2d(plan->fft, grid, false, plan->stream, status);
-        timing_mark(plan, 3);
+        grid_to_image<T>(plan, ip, plane, grid, dirty, status);
         if (*status) return;
-        int e = plan->do_wstacking ?
-                sdp_es::screen_accumulate<T>(ip, plane, grid, dirty,
-                        plan->stream) :
-                sdp_es::screen_corr_2d<T>(ip, grid, dirty, plan->stream);
-        if (plan->do_wstacking &&
-                plane == plan->num_total_w_grids - 1 && !e)
+        if (plan->do_wstacking && plane == plan->num_total_w_grids - 1)
         {
-            e = sdp_es::apply_correction<T>(ip, dirty, plan->stream);
+            const int e = sdp_es::apply_correction<T>(ip, dirty, plan->stream);
+            if (e) { *status = (sdp_Error)e; return; }
         }
-        if (e) { *status = (sdp_Error)e; return; }
         timing_mark(plan, 4);
         timing_collect(plan, kGridSlots);
     }
@@ -343,11 +403,7 @@ void run_degrid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
                 &n_items);
         if (e) { *status = (sdp_Error)e; return; }
         timing_mark(plan, 1);
-        e = sdp_es::reverse_screen<T>(ip, plane, dirty,
-                !plan->do_wstacking, grid, plan->stream);
-        if (e) { *status = (sdp_Error)e; return; }
-        timing_mark(plan, 2);
-        sdp_fft::exec_2d(plan->fft, grid, true, plan->stream, status);
+        image_to_grid<T>(plan, ip, plane, dirty, grid, status);
         if (*status) return;
         timing_mark(plan, 3);
         e = sdp_es::gather<T>(p, plan->scratch, n_items, grid, vis,
@@ -387,6 +443,7 @@ void sdp_gridder_uvw_es_fft_free_plan(sdp_GridderUvwEsFft* plan)
     if (s.recs) (void)hipFree(s.recs);
     if (s.totals_host) (void)hipHostFree(s.totals_host);
     sdp_fft::destroy_2d(plan->fft);
+    sdp_es::fft_twiddles_destroy(&plan->fft_tw);
     if (plan->timing)
         for (int k = 0; k < 5; ++k) (void)hipEventDestroy(plan->ev[k]);
     free(plan);
@@ -511,8 +568,22 @@ sdp_GridderUvwEsFft* sdp_gridder_uvw_es_fft_create_plan(
     }
     ensure_scratch(plan,
             (int64_t)plan->num_rows * plan->num_chan, status);
-    plan->fft = sdp_fft::create_2d(plan->grid_size, plan->grid_size,
-            plan->is_double != 0, status);
+    // SDP_ES_FFT=rocfft keeps rocFFT + separate screen kernels for f32 too.
+    const char* fft_env = getenv("SDP_ES_FFT");
+    plan->fused_fft = !plan->is_double &&
+            sdp_es::fused_fft_supported(plan->grid_size) &&
+            !(fft_env && strcmp(fft_env, "rocfft") == 0);
+    if (plan->fused_fft)
+    {
+        const int e = sdp_es::fft_twiddles_create(plan->grid_size,
+                &plan->fft_tw);
+        if (e && !*status) *status = (sdp_Error)e;
+    }
+    else
+    {
+        plan->fft = sdp_fft::create_2d(plan->grid_size, plan->grid_size,
+                plan->is_double != 0, status);
+    }
     if (*status)
     {
         if (*status == SDP_ERR_RUNTIME) *status = SDP_ERR_MEM_ALLOC_FAILURE;
@@ -623,6 +694,11 @@ double sdp_gridder_uvw_es_fft_beta(const sdp_GridderUvwEsFft* plan)
     return plan ? plan->beta : 0.0;
 }
 
+int sdp_gridder_uvw_es_fft_fused_fft(const sdp_GridderUvwEsFft* plan)
+{
+    return plan ? plan->fused_fft : 0;
+}
+
 void sdp_gridder_uvw_es_fft_set_stream(sdp_GridderUvwEsFft* plan,
         void* hip_stream)
 {
@@ -730,16 +806,12 @@ void sdp_grid_uvw_es_fft_finish(sdp_GridderUvwEsFft* plan, sdp_Mem* grid,
     void* p_grid = sdp_mem_gpu_buffer(grid, status);
     void* p_dirty = sdp_mem_gpu_buffer(dirty_image, status);
     if (*status) return;
-    sdp_fft::exec_2d(plan->fft, *(void**)p_grid, false, plan->stream, status);
-    if (*status) return;
-    int e = 0;
     if (plan->is_double)
-        e = sdp_es::screen_corr_2d<double>(image_params<double>(plan),
-                *(double**)p_grid, *(double**)p_dirty, plan->stream);
+        grid_to_image<double>(plan, image_params<double>(plan), 0,
+                *(double**)p_grid, *(double**)p_dirty, status);
     else
-        e = sdp_es::screen_corr_2d<float>(image_params<float>(plan),
-                *(float**)p_grid, *(float**)p_dirty, plan->stream);
-    if (e) *status = (sdp_Error)e;
+        grid_to_image<float>(plan, image_params<float>(plan), 0,
+                *(float**)p_grid, *(float**)p_dirty, status);
 }
 
 } // extern "C"

@@ -134,6 +134,12 @@ class GridderUvwEsFft(StructWrapper):
         """Full ES kernel beta."""
         return Lib.sdp_gridder_uvw_es_fft_beta(self)
 
+    @property
+    def fused_fft(self):
+        """True if the plan uses the pruned, fused FFT passes (f32,
+        power-of-two grid); False for rocFFT + separate screen kernels."""
+        return bool(Lib.sdp_gridder_uvw_es_fft_fused_fft(self))
+
     def set_stream(self, hip_stream_handle):
         """Launch on the given hipStream_t (int handle; 0 = null stream)."""
         Lib.sdp_gridder_uvw_es_fft_set_stream(
@@ -181,6 +187,8 @@ for _name in ("grid_size", "support", "num_w_planes"):
     Lib.wrap_func(f"sdp_gridder_uvw_es_fft_{_name}", restype=ctypes.c_int,
                   argtypes=[_H])
 Lib.wrap_func("sdp_gridder_uvw_es_fft_beta", restype=ctypes.c_double,
+              argtypes=[_H])
+Lib.wrap_func("sdp_gridder_uvw_es_fft_fused_fft", restype=ctypes.c_int,
               argtypes=[_H])
 Lib.wrap_func("sdp_gridder_uvw_es_fft_set_stream", restype=None,
               argtypes=[_H, ctypes.c_void_p])
