@@ -452,17 +452,49 @@ struct Buf
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(V, x), rsrc,
                 voff, soff, 0);
     }
+
+    // Predicated forms without branches: a disabled lane addresses past
+    // num_records, so the hardware range check returns 0 / drops the store
+    // (a branch per element would make the compiler wait for each load).
+    __device__ __forceinline__ float2 load_if(bool ok, uint32_t voff) const
+    {
+        return load(ok ? voff : kOutOfRange, 0);
+    }
+
+    __device__ __forceinline__ void store_if(bool ok, float2 x,
+            uint32_t voff) const
+    {
+        store(x, ok ? voff : kOutOfRange, 0);
+    }
+
+    static constexpr uint32_t kOutOfRange = 0xFFFFFFF0u;
 };
 
-// 1 / correction of the 2-D path (img::inv_correction without its 3-D
-// branch; same operation order).
-__device__ __forceinline__ float inv_corr_2d(const ImageParams<float>& ip,
-        int i, int j)
+// Same for 32-bit floats (the image).
+struct BufF
 {
-#pragma clang fp contract(off)
-    const float corr = ip.conv_corr[i] * ip.conv_corr[j] * ip.norm * ip.norm;
-    return 1.0f / corr;
-}
+    __amdgpu_buffer_rsrc_t rsrc;
+
+    __device__ __forceinline__ BufF(const void* base, uint32_t bytes)
+    {
+        rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0,
+                (int)bytes, 0x00020000);
+    }
+
+    __device__ __forceinline__ float load_if(bool ok, uint32_t voff) const
+    {
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                rsrc, ok ? voff : Buf::kOutOfRange, 0, 0));
+    }
+
+    __device__ __forceinline__ void store_if(bool ok, float x,
+            uint32_t voff) const
+    {
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(
+                decltype(__builtin_amdgcn_raw_buffer_load_b32(rsrc, 0, 0, 0)),
+                x), rsrc, ok ? voff : Buf::kOutOfRange, 0, 0);
+    }
+};
 
 // Gridding ------------------------------------------------------------------
 //
@@ -496,10 +528,9 @@ k_rows_grid(float2* __restrict__ grid, int k0, int M,
         float2 v[F::EPT];
         F::load_input(v, [&](int c) { return gb.load(vo, ro + c * 8u); });
         f.transform(v, pq, lds, RowIdx{});
-        const uint32_t rs = (uint32_t)row * G * 8u;
+        const uint32_t vr = (uint32_t)row * G * 8u + vo;
         F::store_output(v, [&](int c, int, float2 x) {
-            if ((unsigned)(pq + c - k0) < (unsigned)M)
-                gb.store(x, vo, rs + c * 8u);
+            gb.store_if((unsigned)(pq + c - k0) < (unsigned)M, x, vr + c * 8u);
         });
     }
 }
@@ -561,6 +592,7 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
     const int k2 = blockIdx.x;
     const int h = M / 2;
     const Buf gb(grid, grid_bytes(G, 0));
+    const BufF db(dirty, (uint32_t)((size_t)ip.N * ip.N * 4));
     F f;
     f.init(p, W, G);
     const int ncb = (M + B - 1) / B;
@@ -577,28 +609,34 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
                       : make_float2(0.f, 0.f);
         });
         f.transform(v, pq, lds, ColIdx<B>{cq});
+        const float ccx = ip.conv_corr[min(abs(col - h), h)];
         F::store_output(v, [&](int e, int, float2 x) {
             const int iy = k2 + N2 * (pq + e) - k0;
-            if (!ok || (unsigned)iy >= (unsigned)M) return;
+            const bool in = ok && (unsigned)iy < (unsigned)M;
             const int ix = col;
             const int xo = ix - h, yo = iy - h;
-            float* d = dirty + (size_t)iy * ip.N + ix;
+            const uint32_t off = ((uint32_t)iy * ip.N + ix) * 4u;
+            float val;
             if constexpr (DO_W)
             {
                 float re, im;
                 phasor(ip, plane, abs(xo), abs(yo), -1.0f, re, im);
-                float val = x.x * re - x.y * im;
-                if ((ix + iy) & 1) val = -val;
-                *d += val;
+                val = x.x * re - x.y * im;
             }
             else
             {
-                float val = x.x;
-                if ((ix + iy) & 1) val = -val;
-                float out = *d + val;
-                out *= inv_corr_2d(ip, abs(xo), abs(yo));
-                *d = out;
+                val = x.x;
             }
+            if ((ix + iy) & 1) val = -val;
+            float out = db.load_if(in, off) + val;
+            if constexpr (!DO_W)
+            {
+                // inv_correction (es_image_dev.h), 2-D branch, same order.
+                const float ccy = ip.conv_corr[min(abs(yo), h)];
+                const float corr = ccx * ccy * ip.norm * ip.norm;
+                out *= 1.0f / corr;
+            }
+            db.store_if(in, out, off);
         });
     }
 }
@@ -624,6 +662,7 @@ k_cols_a_image(float* __restrict__ dirty, int correct_in_place,
     const int n1 = blockIdx.x;
     const int h = M / 2;
     const Buf gb(grid, grid_bytes(G, 0));
+    const BufF db(dirty, (uint32_t)((size_t)ip.N * ip.N * 4));
     F f;
     f.init(p, W, G);
     float2 fs[F::EPT];
@@ -638,21 +677,24 @@ k_cols_a_image(float* __restrict__ dirty, int correct_in_place,
         const int col = cb * B + cq;
         const bool ok = col < M;
         float2 v[F::EPT];
+        const float ccx = ip.conv_corr[min(abs(col - h), h)];
         F::load_input(v, [&](int e) {
             const int iy = n1 + N1 * (pq + e) - k0;
-            if (!ok || (unsigned)iy >= (unsigned)M)
-                return make_float2(0.f, 0.f);
+            const bool in = ok && (unsigned)iy < (unsigned)M;
             const int ix = col;
             const int xo = ix - h, yo = iy - h;
-            float* d = dirty + (size_t)iy * ip.N + ix;
-            float val = *d;
+            const uint32_t off = ((uint32_t)iy * ip.N + ix) * 4u;
+            float val = db.load_if(in, off);
             if constexpr (!DO_W)
             {
                 // The 3-D path corrects the whole image before the planes.
                 if (correct_in_place)
                 {
-                    val *= inv_corr_2d(ip, abs(xo), abs(yo));
-                    *d = val;
+                    // inv_correction (es_image_dev.h), 2-D branch.
+                    const float ccy = ip.conv_corr[min(abs(yo), h)];
+                    const float corr = ccx * ccy * ip.norm * ip.norm;
+                    val *= 1.0f / corr;
+                    db.store_if(in, val, off);
                 }
             }
             if ((ix + iy) & 1) val = -val;
@@ -722,9 +764,10 @@ k_rows_image(float2* __restrict__ grid, int k0, int M,
         const uint32_t vo = (uint32_t)pq * 8u;
         const uint32_t rs = (uint32_t)row * G * 8u;
         float2 v[F::EPT];
+        const uint32_t vr = rs + vo;
         F::load_input(v, [&](int c) {
-            return ((unsigned)(pq + c - k0) < (unsigned)M) ?
-                    gb.load(vo, rs + c * 8u) : make_float2(0.f, 0.f);
+            return gb.load_if((unsigned)(pq + c - k0) < (unsigned)M,
+                    vr + c * 8u);
         });
         f.transform(v, pq, lds, RowIdx{});
         const uint32_t ro = ((uint32_t)row * G + k0) * 8u;
