@@ -184,7 +184,6 @@ def main():
     plan = GridderUvwEsFft(uvw, freq, vis, weight, dirty, px, px, args.eps,
                            False)
     plan.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    plan.enable_timing(True)
     G, W = plan.grid_size, plan.support
     grid_buf = None
     if world > 1 and args.reduce == "grid":
@@ -210,14 +209,9 @@ def main():
     for _ in range(args.warmup):
         grid_step()
     barrier()
-    phases = {"bucket": 0.0, "tile_kernel": 0.0, "fft": 0.0, "image": 0.0}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         grid_step()
-        tm = plan.get_timing()
-        if tm:
-            for k in phases:
-                phases[k] += tm[k]
     barrier()
     t_grid = time.perf_counter() - t0
     if dist is not None:
@@ -227,7 +221,20 @@ def main():
     ms_per_step = 1e3 * t_grid / args.steps
     total_vis = args.rows * args.chan * world
     value = total_vis * args.steps / t_grid / 1e6
-    avg = {k: v / args.steps for k, v in phases.items()}
+
+    # Per-phase device times (HIP events on the plan stream), in separate
+    # calls so that the event synchronisation stays out of the timed loop.
+    phase_steps = max(1, min(args.steps, 5))
+    plan.enable_timing(True)
+    phases = {"bucket": 0.0, "tile_kernel": 0.0, "fft": 0.0, "image": 0.0}
+    for _ in range(phase_steps):
+        grid_step()
+        tm = plan.get_timing()
+        for k in phases:
+            phases[k] += tm[k] if tm else 0.0
+    plan.enable_timing(False)
+    barrier()
+    avg = {k: v / phase_steps for k, v in phases.items()}
 
     # Degridding half of the round trip (same image, same step count).
     degrid = None
@@ -239,25 +246,30 @@ def main():
             img.copy_(image0)
             plan.ifft_grid_uvw_es(uvw, freq, out_vis, weight, img)
         barrier()
-        dph = {"bucket": 0.0, "tile_kernel": 0.0, "fft": 0.0, "image": 0.0}
         t0 = time.perf_counter()
         for _ in range(args.steps):
             img.copy_(image0)
             plan.ifft_grid_uvw_es(uvw, freq, out_vis, weight, img)
-            tm = plan.get_timing()
-            if tm:
-                for k in dph:
-                    dph[k] += tm[k]
         barrier()
         t_deg = time.perf_counter() - t0
         if dist is not None:
             t = torch.tensor([t_deg], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             t_deg = float(t.item())
+        dph = {"bucket": 0.0, "tile_kernel": 0.0, "fft": 0.0, "image": 0.0}
+        plan.enable_timing(True)
+        for _ in range(phase_steps):
+            img.copy_(image0)
+            plan.ifft_grid_uvw_es(uvw, freq, out_vis, weight, img)
+            tm = plan.get_timing()
+            for k in dph:
+                dph[k] += tm[k] if tm else 0.0
+        plan.enable_timing(False)
+        barrier()
         degrid = {
             "mvis_s": total_vis * args.steps / t_deg / 1e6,
             "ms_per_step": 1e3 * t_deg / args.steps,
-            "phases_ms": {k: v / args.steps for k, v in dph.items()},
+            "phases_ms": {k: round(v / phase_steps, 4) for k, v in dph.items()},
         }
 
     # Roofline of the dominant kernel of a gridding call.
@@ -271,9 +283,11 @@ def main():
     achieved = (kern_bytes[dom] / (avg[dom] * 1e-3) / 1e9
                 if avg.get(dom) else None)
     kernel_names = {"tile_kernel": "k_scatter_mfma (MFMA tile accumulation)",
-                    "fft": "rocFFT 2-D C2C inverse",
+                    "fft": ("k_rows_grid + k_cols_a_grid (pruned FFT passes)"
+                            if plan.fused_fft else "rocFFT 2-D C2C inverse"),
                     "bucket": "bucketing (count/scan/fill)",
-                    "image": "k_screen_corr_2d"}
+                    "image": ("k_cols_b_grid (last FFT pass + screen)"
+                              if plan.fused_fft else "k_screen_corr_2d")}
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):

@@ -1,8 +1,7 @@
 // HIP kernels of the MI355X-native ES-FFT (de)gridder: launch interface.
 //
 // Data path (one w-plane, one call):
-//   bucket_count -> scan_columns -> scan_bins -> [host reads 2 totals]
-//   -> bucket_fill -> (grid) zero_hot_tiles + scatter_tiles
+//   bucket_count -> scan_columns -> scan_bins -> bucket_fill -> (grid) zero_hot_tiles + scatter_tiles
 //                     (degrid) gather_tiles
 // Visibilities are bucketed by 64x64 grid tile (counting sort, LDS-private
 // histograms per chunk of visibilities). In grid mode a visibility is listed
@@ -55,8 +54,7 @@ struct BucketScratch
     uint32_t* totals = nullptr;     // [2]: entries, items
     uint32_t* item_bin = nullptr;   // [item_capacity]: work item -> bin
     uint32_t item_capacity = 0;
-    uint32_t* totals_host = nullptr;// pinned host mirror of totals
-    void* recs = nullptr;           // bucketed records
+    void* recs = nullptr;           // bucketed records (worst-case size)
     size_t recs_bytes = 0;
     size_t table_entries = 0;
 };
@@ -64,8 +62,10 @@ struct BucketScratch
 // Number of visibility chunks used for a given visibility count.
 int num_chunks(int64_t num_vis);
 
-// Bucketing: returns host-visible totals (entries, items) after a stream
-// sync; fills scratch.recs (re-allocated if too small). Record layouts:
+// Bucketing, fully asynchronous: fills scratch.recs (sized by the caller
+// for the worst case, 4 entries per visibility) and the work-item table;
+// *n_items is the launch bound item_capacity (work items past the real
+// count find kNoBin and exit), *n_entries is 0. Record layouts:
 //   grid, 2-D:  {pu, pv, vre*w, vim*w}
 //   grid, 3-D:  {pu, pv, vre*w, vim*w*flip, kw, 0, 0, 0}
 //   degrid:     {pu, pv, kw*flip (sign carries flip), index bits}

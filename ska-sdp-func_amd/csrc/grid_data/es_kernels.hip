@@ -6,6 +6,7 @@
 // up to the libm exp/sqrt ulp; only the summation ORDER differs (LDS tile
 // accumulation instead of per-tap HBM atomics).
 #include <cmath>
+#include <cstdlib>
 
 #include "es_kernels.h"
 #include "es_params.h"
@@ -145,47 +146,50 @@ __device__ __forceinline__ uint64_t bits_idx(double x)
 
 // Bucketing kernels ---------------------------------------------------------
 
-template<typename T, int MODE>
-__global__ __launch_bounds__(kThreads) void k_bucket_count(EsParams<T> p,
-        int64_t num_vis, int num_chan, int64_t chunk, const T* __restrict__ uvw,
+template<typename T, int MODE, int NT>
+__global__ __launch_bounds__(NT) void k_bucket_count(EsParams<T> p,
+        int64_t num_rows, int num_chan, int64_t chunk, const T* __restrict__ uvw,
         const T* __restrict__ freq, uint32_t* __restrict__ table)
 {
     __shared__ uint32_t hist[kBinsPerPass];
     const int pass_base = blockIdx.y * kBinsPerPass;
     const int nb = min(kBinsPerPass, p.nbins - pass_base);
-    for (int i = threadIdx.x; i < nb; i += kThreads) hist[i] = 0;
+    for (int i = threadIdx.x; i < nb; i += NT) hist[i] = 0;
     __syncthreads();
-    const int64_t i0 = (int64_t)blockIdx.x * chunk;
-    const int64_t i1 = min(num_vis, i0 + chunk);
+    // Chunks are ranges of rows; a thread takes a row and its channels
+    // (no 64-bit division per visibility, uvw read once per row).
+    const int64_t r0 = (int64_t)blockIdx.x * chunk;
+    const int64_t r1 = min(num_rows, r0 + chunk);
     const int half = p.G / 2;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += kThreads)
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += NT)
     {
-        const int64_t r = i / num_chan;
-        const int c = (int)(i - r * num_chan);
-        Footprint<T> f;
-        if (!footprint(p, uvw[3 * r], uvw[3 * r + 1], uvw[3 * r + 2], freq[c],
-                f)) continue;
-        if (MODE == MODE_GRID)
+        const T u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2];
+        for (int c = 0; c < num_chan; ++c)
         {
-            const int tu0 = (f.u0 + half) / kTile, tu1 = (f.u1 + half) / kTile;
-            const int tv0 = (f.v0 + half) / kTile, tv1 = (f.v1 + half) / kTile;
-            for (int tu = tu0; tu <= tu1; ++tu)
-                for (int tv = tv0; tv <= tv1; ++tv)
-                {
-                    const int b = tu * p.ntiles + tv - pass_base;
-                    if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
-                }
-        }
-        else
-        {
-            const int b = ((f.u0 + half) / kTile) * p.ntiles +
-                    (f.v0 + half) / kTile - pass_base;
-            if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
+            Footprint<T> f;
+            if (!footprint(p, u, v, w, freq[c], f)) continue;
+            if (MODE == MODE_GRID)
+            {
+                const int tu0 = (f.u0 + half) / kTile, tu1 = (f.u1 + half) / kTile;
+                const int tv0 = (f.v0 + half) / kTile, tv1 = (f.v1 + half) / kTile;
+                for (int tu = tu0; tu <= tu1; ++tu)
+                    for (int tv = tv0; tv <= tv1; ++tv)
+                    {
+                        const int b = tu * p.ntiles + tv - pass_base;
+                        if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
+                    }
+            }
+            else
+            {
+                const int b = ((f.u0 + half) / kTile) * p.ntiles +
+                        (f.v0 + half) / kTile - pass_base;
+                if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
+            }
         }
     }
     __syncthreads();
     uint32_t* row = table + (size_t)blockIdx.x * p.nbins + pass_base;
-    for (int i = threadIdx.x; i < nb; i += kThreads) row[i] = hist[i];
+    for (int i = threadIdx.x; i < nb; i += NT) row[i] = hist[i];
 }
 
 // Per bin: exclusive prefix over chunks (in place) and the bin total.
@@ -229,60 +233,135 @@ __global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
 }
 
 // Exclusive prefix of bin totals and of work items (pieces of <= kPiece
-// entries, at least one per bin). One block of 1024 threads.
+// entries, at least one per bin), the work item -> bin table, and the
+// sentinel kNoBin in item_bin past the last item (tile kernels are
+// launched for item_capacity work items and the extra ones exit: no host
+// round trip for the item count). One block of 1024 threads; rounds of
+// 16 consecutive bins per thread, loaded with 16-byte loads.
+constexpr uint32_t kNoBin = 0xFFFFFFFFu;
+
+__device__ __forceinline__ void block_scan_1024(uint32_t& a, uint32_t& b,
+        uint32_t* s_a, uint32_t* s_b, uint32_t& tot_a, uint32_t& tot_b)
+{
+    // Inclusive scan of (a, b) over the block; returns exclusive values and
+    // the block totals.
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t ia = a, ib = b;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1)
+    {
+        const uint32_t xa = __shfl_up(ia, off), xb = __shfl_up(ib, off);
+        if (lane >= off) { ia += xa; ib += xb; }
+    }
+    if (lane == 63) { s_a[wave] = ia; s_b[wave] = ib; }
+    __syncthreads();
+    if (wave == 0)
+    {
+        uint32_t wa = lane < 16 ? s_a[lane] : 0, wb = lane < 16 ? s_b[lane] : 0;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1)
+        {
+            const uint32_t xa = __shfl_up(wa, off), xb = __shfl_up(wb, off);
+            if (lane >= off) { wa += xa; wb += xb; }
+        }
+        if (lane < 16) { s_a[16 + lane] = wa; s_b[16 + lane] = wb; }
+    }
+    __syncthreads();
+    const uint32_t pa = wave ? s_a[16 + wave - 1] : 0;
+    const uint32_t pb = wave ? s_b[16 + wave - 1] : 0;
+    tot_a = s_a[31];
+    tot_b = s_b[31];
+    a = pa + ia - a;
+    b = pb + ib - b;
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(1024) void k_scan_bins(
         const uint32_t* __restrict__ bin_count, int nbins,
         uint32_t* __restrict__ bin_start, uint32_t* __restrict__ item_start,
         uint32_t* __restrict__ totals, uint32_t* __restrict__ item_bin,
         uint32_t item_capacity)
 {
-    __shared__ uint32_t s_cnt[1024], s_itm[1024];
+    __shared__ uint32_t s_a[32], s_b[32];
+    constexpr int kPer = 16;
     const int t = threadIdx.x;
-    const int per = (nbins + 1023) / 1024;
-    const int b0 = min(nbins, t * per), b1 = min(nbins, b0 + per);
-    uint32_t cnt = 0, itm = 0;
-    for (int b = b0; b < b1; ++b)
+    uint32_t carry_c = 0, carry_i = 0;
+    for (int base = 0; base < nbins; base += 1024 * kPer)
     {
-        const uint32_t n = bin_count[b];
-        cnt += n;
-        itm += max(1u, (n + kPiece - 1) / kPiece);
+        const int b0 = base + t * kPer;
+        uint32_t n[kPer];
+        if (b0 + kPer <= nbins)
+        {
+            const uint4* src = (const uint4*)(bin_count + b0);
+#pragma unroll
+            for (int k = 0; k < kPer / 4; ++k)
+            {
+                const uint4 v = src[k];
+                n[4 * k] = v.x; n[4 * k + 1] = v.y;
+                n[4 * k + 2] = v.z; n[4 * k + 3] = v.w;
+            }
+        }
+        else
+        {
+#pragma unroll
+            for (int k = 0; k < kPer; ++k)
+                n[k] = (b0 + k < nbins) ? bin_count[b0 + k] : 0;
+        }
+        uint32_t cnt = 0, itm = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+        {
+            cnt += n[k];
+            if (b0 + k < nbins) itm += max(1u, (n[k] + kPiece - 1) / kPiece);
+        }
+        uint32_t tot_c, tot_i;
+        block_scan_1024(cnt, itm, s_a, s_b, tot_c, tot_i);
+        uint32_t run_c = carry_c + cnt, run_i = carry_i + itm;
+        for (int k = 0; k < kPer; ++k)
+        {
+            const int bb = b0 + k;
+            if (bb >= nbins) break;
+            const uint32_t ni = max(1u, (n[k] + kPiece - 1) / kPiece);
+            bin_start[bb] = run_c;
+            item_start[bb] = run_i;
+            for (uint32_t j = 0; j < ni; ++j)
+                if (run_i + j < item_capacity) item_bin[run_i + j] = (uint32_t)bb;
+            run_c += n[k];
+            run_i += ni;
+        }
+        carry_c += tot_c;
+        carry_i += tot_i;
     }
-    s_cnt[t] = cnt;
-    s_itm[t] = itm;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1)   // inclusive Hillis-Steele
+    if (t == 0)
     {
-        const uint32_t a = (t >= off) ? s_cnt[t - off] : 0;
-        const uint32_t c = (t >= off) ? s_itm[t - off] : 0;
-        __syncthreads();
-        s_cnt[t] += a;
-        s_itm[t] += c;
-        __syncthreads();
+        bin_start[nbins] = carry_c;
+        item_start[nbins] = carry_i;
+        totals[0] = carry_c;
+        totals[1] = carry_i;
     }
-    uint32_t run_c = s_cnt[t] - cnt, run_i = s_itm[t] - itm;
-    for (int b = b0; b < b1; ++b)
+    for (uint32_t k = carry_i + t; k < item_capacity; k += 1024)
+        item_bin[k] = kNoBin;
+}
+
+// One bucketed record as 16-byte stores (records are 16-byte aligned).
+template<typename T, int W>
+__device__ __forceinline__ void store_rec(T* dst, const T (&rec)[W])
+{
+    constexpr int kPer = 16 / sizeof(T);
+    using V = __attribute__((ext_vector_type(kPer))) T;
+#pragma unroll
+    for (int k = 0; k < W; k += kPer)
     {
-        const uint32_t n = bin_count[b];
-        const uint32_t ni = max(1u, (n + kPiece - 1) / kPiece);
-        bin_start[b] = run_c;
-        item_start[b] = run_i;
-        for (uint32_t k = 0; k < ni; ++k)
-            if (run_i + k < item_capacity) item_bin[run_i + k] = (uint32_t)b;
-        run_c += n;
-        run_i += ni;
-    }
-    if (t == 1023)
-    {
-        bin_start[nbins] = s_cnt[1023];
-        item_start[nbins] = s_itm[1023];
-        totals[0] = s_cnt[1023];
-        totals[1] = s_itm[1023];
+        V x;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) x[j] = rec[k + j];
+        *(V*)(dst + k) = x;
     }
 }
 
-template<typename T, int MODE, bool DO_W>
-__global__ __launch_bounds__(kThreads) void k_bucket_fill(EsParams<T> p,
-        int64_t num_vis, int num_chan, int64_t chunk, const T* __restrict__ uvw,
+template<typename T, int MODE, bool DO_W, int NT>
+__global__ __launch_bounds__(NT) void k_bucket_fill(EsParams<T> p,
+        int64_t num_rows, int num_chan, int64_t chunk, const T* __restrict__ uvw,
         const T* __restrict__ freq, const T* __restrict__ vis,
         const T* __restrict__ weight, const uint32_t* __restrict__ table,
         const uint32_t* __restrict__ bin_start, T* __restrict__ recs)
@@ -292,59 +371,57 @@ __global__ __launch_bounds__(kThreads) void k_bucket_fill(EsParams<T> p,
     const int pass_base = blockIdx.y * kBinsPerPass;
     const int nb = min(kBinsPerPass, p.nbins - pass_base);
     const uint32_t* row = table + (size_t)blockIdx.x * p.nbins + pass_base;
-    for (int i = threadIdx.x; i < nb; i += kThreads)
+    for (int i = threadIdx.x; i < nb; i += NT)
         cursor[i] = bin_start[pass_base + i] + row[i];
     __syncthreads();
-    const int64_t i0 = (int64_t)blockIdx.x * chunk;
-    const int64_t i1 = min(num_vis, i0 + chunk);
+    const int64_t r0 = (int64_t)blockIdx.x * chunk;
+    const int64_t r1 = min(num_rows, r0 + chunk);
     const int half = p.G / 2;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += kThreads)
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += NT)
     {
-        const int64_t r = i / num_chan;
-        const int c = (int)(i - r * num_chan);
-        Footprint<T> f;
-        if (!footprint(p, uvw[3 * r], uvw[3 * r + 1], uvw[3 * r + 2], freq[c],
-                f)) continue;
-        T rec[kWords];
-        rec[0] = f.pu;
-        rec[1] = f.pv;
-        if constexpr (MODE == MODE_GRID)
+        const T u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2];
+        for (int c = 0; c < num_chan; ++c)
         {
-            // kernels.cu:163-167: weight, then conjugate for w < 0.
-            const T wt = weight[i];
-            rec[2] = vis[2 * i] * wt;
-            T vim = vis[2 * i + 1] * wt;
-            vim *= f.flip;
-            rec[3] = vim;
-            if constexpr (DO_W && kWords == 8)
+            const int64_t i = r * num_chan + c;
+            Footprint<T> f;
+            if (!footprint(p, u, v, w, freq[c], f)) continue;
+            T rec[kWords];
+            rec[0] = f.pu;
+            rec[1] = f.pv;
+            if constexpr (MODE == MODE_GRID)
             {
-                rec[4] = f.kw;
-                rec[5] = rec[6] = rec[7] = T(0);
-            }
-            const int tu0 = (f.u0 + half) / kTile, tu1 = (f.u1 + half) / kTile;
-            const int tv0 = (f.v0 + half) / kTile, tv1 = (f.v1 + half) / kTile;
-            for (int tu = tu0; tu <= tu1; ++tu)
-                for (int tv = tv0; tv <= tv1; ++tv)
+                // kernels.cu:163-167: weight, then conjugate for w < 0.
+                const T wt = weight[i];
+                rec[2] = vis[2 * i] * wt;
+                T vim = vis[2 * i + 1] * wt;
+                vim *= f.flip;
+                rec[3] = vim;
+                if constexpr (DO_W && kWords == 8)
                 {
-                    const int b = tu * p.ntiles + tv - pass_base;
-                    if (b < 0 || b >= nb) continue;
-                    const uint32_t pos = atomicAdd(&cursor[b], 1u);
-                    T* dst = recs + (size_t)pos * kWords;
-#pragma unroll
-                    for (int k = 0; k < kWords; ++k) dst[k] = rec[k];
+                    rec[4] = f.kw;
+                    rec[5] = rec[6] = rec[7] = T(0);
                 }
-        }
-        else
-        {
-            rec[2] = copysign(f.kw, f.flip);
-            rec[3] = idx_bits(T(0), (uint64_t)i);
-            const int b = ((f.u0 + half) / kTile) * p.ntiles +
-                    (f.v0 + half) / kTile - pass_base;
-            if (b < 0 || b >= nb) continue;
-            const uint32_t pos = atomicAdd(&cursor[b], 1u);
-            T* dst = recs + (size_t)pos * kWords;
-#pragma unroll
-            for (int k = 0; k < kWords; ++k) dst[k] = rec[k];
+                const int tu0 = (f.u0 + half) / kTile, tu1 = (f.u1 + half) / kTile;
+                const int tv0 = (f.v0 + half) / kTile, tv1 = (f.v1 + half) / kTile;
+                for (int tu = tu0; tu <= tu1; ++tu)
+                    for (int tv = tv0; tv <= tv1; ++tv)
+                    {
+                        const int b = tu * p.ntiles + tv - pass_base;
+                        if (b < 0 || b >= nb) continue;
+                        const uint32_t pos = atomicAdd(&cursor[b], 1u);
+                        store_rec<T, kWords>(recs + (size_t)pos * kWords, rec);
+                    }
+            }
+            else
+            {
+                rec[2] = copysign(f.kw, f.flip);
+                rec[3] = idx_bits(T(0), (uint64_t)i);
+                const int b = ((f.u0 + half) / kTile) * p.ntiles +
+                        (f.v0 + half) / kTile - pass_base;
+                if (b < 0 || b >= nb) continue;
+                const uint32_t pos = atomicAdd(&cursor[b], 1u);
+                store_rec<T, kWords>(recs + (size_t)pos * kWords, rec);
+            }
         }
     }
 }
@@ -470,6 +547,7 @@ __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
         s_im[k] = T(0);
     }
     const uint32_t item = blockIdx.x;
+    if (item_bin[item] == kNoBin) return;   // past the last work item
     const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
     const uint32_t npieces = item_start[b + 1] - item_start[b];
@@ -672,6 +750,7 @@ __global__ __launch_bounds__(256) void k_scatter_mfma(EsParams<float> p,
     __shared__ VisitPool<4> s_vp;
 
     const uint32_t item = blockIdx.x;
+    if (item_bin[item] == kNoBin) return;   // past the last work item
     const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
     const uint32_t npieces = item_start[b + 1] - item_start[b];
@@ -826,6 +905,7 @@ __global__ __launch_bounds__(256) void k_gather_mfma(EsParams<float> p,
     __shared__ VisitPool<kSub> s_vp;
 
     const uint32_t item = blockIdx.x;
+    if (item_bin[item] == kNoBin) return;   // past the last work item
     const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
     const uint32_t e0 = bin_start[b] + piece * kPiece;
@@ -965,6 +1045,7 @@ __global__ __launch_bounds__(kThreads) void k_gather(EsParams<T> p,
     T* w_re = (T*)smem;
     T* w_im = w_re + wrows * ws;
     const uint32_t item = blockIdx.x;
+    if (item_bin[item] == kNoBin) return;   // past the last work item
     const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
     const uint32_t e0 = bin_start[b] + piece * kPiece;
@@ -1174,11 +1255,63 @@ dim3 image_blocks(int n)
 
 } // namespace
 
+// Visibilities per bucketing chunk (env SDP_ES_CHUNK_VIS for experiments).
+int64_t chunk_vis()
+{
+    static int64_t v = 0;
+    if (!v)
+    {
+        const char* e = getenv("SDP_ES_CHUNK_VIS");
+        v = e ? std::max<int64_t>(256, atoll(e)) : 8192;
+    }
+    return v;
+}
+
+int bucket_threads()
+{
+    static int v = 0;
+    if (!v)
+    {
+        const char* e = getenv("SDP_ES_BUCKET_THREADS");
+        v = e ? atoi(e) : 1024;
+        if (v != 256 && v != 512 && v != 1024) v = 256;
+    }
+    return v;
+}
+
 int num_chunks(int64_t num_vis)
 {
-    const int64_t by_size = (num_vis + 8191) / 8192;
+    const int64_t cv = chunk_vis();
+    const int64_t by_size = (num_vis + cv - 1) / cv;
     return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxChunks, by_size));
 }
+
+template<typename T, int MODE, int NT>
+void launch_count(const dim3& g, const EsParams<T>& p, int64_t num_rows,
+        int num_chan, int64_t chunk, const T* uvw, const T* freq,
+        uint32_t* table, hipStream_t stream)
+{
+    k_bucket_count<T, MODE, NT><<<g, NT, 0, stream>>>(p, num_rows, num_chan,
+            chunk, uvw, freq, table);
+}
+
+template<typename T, int MODE, bool DO_W, int NT>
+void launch_fill(const dim3& g, const EsParams<T>& p, int64_t num_rows,
+        int num_chan, int64_t chunk, const T* uvw, const T* freq, const T* vis,
+        const T* weight, const uint32_t* table, const uint32_t* bin_start,
+        T* recs, hipStream_t stream)
+{
+    k_bucket_fill<T, MODE, DO_W, NT><<<g, NT, 0, stream>>>(p, num_rows,
+            num_chan, chunk, uvw, freq, vis, weight, table, bin_start, recs);
+}
+
+#define SDP_ES_BY_THREADS(NTV, CALL) \
+    switch (NTV) \
+    { \
+    case 1024: { constexpr int NT = 1024; CALL; break; } \
+    case 512:  { constexpr int NT = 512;  CALL; break; } \
+    default:   { constexpr int NT = 256;  CALL; break; } \
+    }
 
 template<typename T>
 int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
@@ -1190,15 +1323,16 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
     sdp_Error* status = &st;
     const int64_t num_vis = num_rows * num_chan;
     const int nc = num_chunks(num_vis);
-    const int64_t chunk = (num_vis + nc - 1) / nc;
+    const int64_t chunk = (num_rows + nc - 1) / nc;   // rows per chunk
     const int passes = (p.nbins + kBinsPerPass - 1) / kBinsPerPass;
     const dim3 grid_b(nc, passes);
+    const int nt = bucket_threads();
     if (mode == MODE_GRID)
-        k_bucket_count<T, MODE_GRID><<<grid_b, kThreads, 0, stream>>>(
-                p, num_vis, num_chan, chunk, uvw, freq, s->table);
+        SDP_ES_BY_THREADS(nt, (launch_count<T, MODE_GRID, NT>(grid_b, p,
+                num_rows, num_chan, chunk, uvw, freq, s->table, stream)))
     else
-        k_bucket_count<T, MODE_DEGRID><<<grid_b, kThreads, 0, stream>>>(
-                p, num_vis, num_chan, chunk, uvw, freq, s->table);
+        SDP_ES_BY_THREADS(nt, (launch_count<T, MODE_DEGRID, NT>(grid_b, p,
+                num_rows, num_chan, chunk, uvw, freq, s->table, stream)))
     SDP_HIP_CHECK_LAUNCH(status);
     k_scan_columns<<<(p.nbins + 63) / 64, 1024, 0, stream>>>(
             s->table, nc, p.nbins, s->bin_count);
@@ -1206,40 +1340,36 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
     k_scan_bins<<<1, 1024, 0, stream>>>(s->bin_count, p.nbins, s->bin_start,
             s->item_start, s->totals, s->item_bin, s->item_capacity);
     SDP_HIP_CHECK_LAUNCH(status);
-    SDP_HIP_CHECK(hipMemcpyAsync(s->totals_host, s->totals,
-            2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream), status);
-    SDP_HIP_CHECK(hipStreamSynchronize(stream), status);
-    if (*status) return *status;
-    *n_entries = s->totals_host[0];
-    *n_items = s->totals_host[1];
+    // No host round trip: records and work items are sized for the worst
+    // case by the caller (BucketScratch::recs_bytes / item_capacity).
     const int words = (mode == MODE_GRID && p.do_w) ? 8 : 4;
-    const size_t need = (size_t)(*n_entries) * words * sizeof(T);
-    if (need > s->recs_bytes)
+    const size_t worst = (size_t)num_vis * (mode == MODE_GRID ? 4 : 1) *
+            words * sizeof(T);
+    if (worst > s->recs_bytes)
     {
-        if (s->recs) SDP_HIP_CHECK(hipFree(s->recs), status);
-        const size_t bytes = need + need / 8 + 4096;
-        s->recs = nullptr;
-        SDP_HIP_CHECK(hipMalloc(&s->recs, bytes), status);
-        if (*status) return SDP_ERR_MEM_ALLOC_FAILURE;
-        s->recs_bytes = bytes;
+        SDP_LOG_ERROR("Bucketing scratch too small (%zu < %zu bytes)",
+                s->recs_bytes, worst);
+        return SDP_ERR_RUNTIME;
     }
+    *n_entries = 0;                  // not known on the host
+    *n_items = s->item_capacity;     // upper bound; extra items exit
     T* recs = (T*)s->recs;
     if (mode == MODE_GRID)
     {
         if (p.do_w)
-            k_bucket_fill<T, MODE_GRID, true><<<grid_b, kThreads, 0, stream>>>(
-                    p, num_vis, num_chan, chunk, uvw, freq, vis, weight,
-                    s->table, s->bin_start, recs);
+            SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_GRID, true, NT>(grid_b,
+                    p, num_rows, num_chan, chunk, uvw, freq, vis, weight,
+                    s->table, s->bin_start, recs, stream)))
         else
-            k_bucket_fill<T, MODE_GRID, false><<<grid_b, kThreads, 0,
-                    stream>>>(p, num_vis, num_chan, chunk, uvw, freq, vis,
-                    weight, s->table, s->bin_start, recs);
+            SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_GRID, false, NT>(grid_b,
+                    p, num_rows, num_chan, chunk, uvw, freq, vis, weight,
+                    s->table, s->bin_start, recs, stream)))
     }
     else
     {
-        k_bucket_fill<T, MODE_DEGRID, false><<<grid_b, kThreads, 0, stream>>>(
-                p, num_vis, num_chan, chunk, uvw, freq, vis, weight,
-                s->table, s->bin_start, recs);
+        SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_DEGRID, false, NT>(grid_b,
+                p, num_rows, num_chan, chunk, uvw, freq, vis, weight,
+                s->table, s->bin_start, recs, stream)))
     }
     SDP_HIP_CHECK_LAUNCH(status);
     return *status;

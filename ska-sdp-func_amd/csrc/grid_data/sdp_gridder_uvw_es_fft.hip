@@ -192,10 +192,12 @@ void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
 {
     if (*status) return;
     sdp_es::BucketScratch& s = plan->scratch;
-    // Work items: at least one per bin, plus one per kPiece entries (a
-    // visibility is listed in at most 4 tiles).
-    const size_t items = 2 * (size_t)plan->nbins + 1 +
-            (size_t)(4 * num_vis) / sdp_es::kPiece;
+    // Worst case, so that bucketing needs no host round trip: a visibility
+    // is listed in at most 4 tiles (support <= 64 < tile), work items are
+    // one per bin plus one per kPiece entries.
+    const size_t max_entries = 4 * (size_t)num_vis;
+    const size_t items = (size_t)plan->nbins + 1 +
+            (max_entries + sdp_es::kPiece - 1) / sdp_es::kPiece;
     if (items > s.item_capacity)
     {
         if (s.item_bin) SDP_HIP_CHECK(hipFree(s.item_bin), status);
@@ -203,6 +205,15 @@ void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
         SDP_HIP_CHECK(hipMalloc(&s.item_bin, items * sizeof(uint32_t)),
                 status);
         s.item_capacity = *status ? 0 : (uint32_t)items;
+    }
+    const size_t words = plan->do_wstacking ? 8 : 4;
+    const size_t rec_bytes = max_entries * words * real_size(plan);
+    if (rec_bytes > s.recs_bytes)
+    {
+        if (s.recs) SDP_HIP_CHECK(hipFree(s.recs), status);
+        s.recs = nullptr;
+        SDP_HIP_CHECK(hipMalloc(&s.recs, rec_bytes), status);
+        s.recs_bytes = *status ? 0 : rec_bytes;
     }
     const size_t need = (size_t)sdp_es::num_chunks(num_vis) * plan->nbins;
     if (need > s.table_entries)
@@ -441,7 +452,6 @@ void sdp_gridder_uvw_es_fft_free_plan(sdp_GridderUvwEsFft* plan)
     if (s.item_bin) (void)hipFree(s.item_bin);
     if (s.bin_count) (void)hipFree(s.bin_count);
     if (s.recs) (void)hipFree(s.recs);
-    if (s.totals_host) (void)hipHostFree(s.totals_host);
     sdp_fft::destroy_2d(plan->fft);
     sdp_es::fft_twiddles_destroy(&plan->fft_tw);
     if (plan->timing)
@@ -563,8 +573,6 @@ sdp_GridderUvwEsFft* sdp_gridder_uvw_es_fft_create_plan(
             s.item_start = s.bin_start + nb + 1;
             s.totals = s.item_start + nb + 1;
         }
-        SDP_HIP_CHECK(hipHostMalloc((void**)&s.totals_host,
-                2 * sizeof(uint32_t), hipHostMallocDefault), status);
     }
     ensure_scratch(plan,
             (int64_t)plan->num_rows * plan->num_chan, status);
