@@ -224,3 +224,38 @@ print("|".join(out))
         "Error 3: Unsupported data type(s)",
         "Error 2: Invalid function argument",
         "Error 6: Memory location mismatch"])
+
+
+# Flagger argument checks (sdp_flagger.cpp:10-57): all raised before any
+# device work, so they run without a GPU.
+def _flag_call(vis, flags, **over):
+    from ska_sdp_func.visibility import flagger_dynamic_threshold
+
+    kw = dict(alpha=0.5, threshold_magnitudes=3.5, threshold_variations=3.5,
+              threshold_broadband=3.5, sampling_step=1, window=0,
+              window_median_history=20)
+    kw.update(over)
+    flagger_dynamic_threshold(vis, flags, **kw)
+
+
+def test_flagger_argument_errors():
+    from ska_sdp_func.utility import CError
+
+    vis = np.ones((4, 2, 8, 1), np.complex64)
+    flags = np.zeros((4, 2, 8, 1), np.int32)
+    with pytest.raises(CError, match="Error 1"):        # not 4-D
+        _flag_call(vis[:, :, :, 0], flags[:, :, :, 0])
+    with pytest.raises(CError, match="Error 1"):        # not contiguous
+        _flag_call(vis[:, :, ::2], flags[:, :, ::2])
+    with pytest.raises(CError, match="Error 3"):        # real vis
+        _flag_call(np.ones((4, 2, 8, 1), np.float32), flags)
+    with pytest.raises(CError, match="Error 3"):        # float flags
+        _flag_call(vis, np.zeros((4, 2, 8, 1), np.float32))
+    with pytest.raises(CError, match="Error 2"):        # shape mismatch
+        _flag_call(vis, np.zeros((4, 2, 7, 1), np.int32))
+    with pytest.raises(CError, match="Error 2"):        # sampling_step 0
+        _flag_call(vis, flags, sampling_step=0)
+    ro = flags.copy()
+    ro.setflags(write=False)
+    with pytest.raises(CError, match="Error 1"):        # read-only flags
+        _flag_call(vis, ro)
