@@ -1,0 +1,168 @@
+/* MI355X-native gridder utilities of the w-towers path: drop-in C ABI.
+ *
+ * The subset of src/ska-sdp-func/grid_data/sdp_gridder_utils.h and
+ * sdp_gridder_clamp_channels.h (ska-sdp-func 1.2.2) that the w-towers
+ * gridder and its tests use; same names, arguments and semantics.
+ * Table generators (make_kernel, make_pswf_kernel, make_w_pattern) fill
+ * host (CPU) arrays, as in the reference; the array operations run on the
+ * GPU for device arrays and stage host arrays through device memory.
+ */
+#ifndef SDP_GRIDDER_UTILS_H_
+#define SDP_GRIDDER_UTILS_H_
+
+#include "ska-sdp-func/utility/sdp_mem.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* out += in1 * in2 ** exponent (in2 may be NULL: out += in1; a real out
+ * takes the real part), sdp_gridder_utils.h:40-46 (impl .cpp:722-852). */
+void sdp_gridder_accumulate_scaled_arrays(
+        sdp_Mem* out,
+        const sdp_Mem* in1,
+        const sdp_Mem* in2,
+        int exponent,
+        sdp_Error* status
+);
+
+/* w step for a field of view, .h:69-75 (impl .cpp:1016-1039). */
+double sdp_gridder_determine_w_step(
+        double theta,
+        double fov,
+        double shear_u,
+        double shear_v,
+        double x0
+);
+
+/* Oversampled uv kernel [oversampling + 1, support] from an image-space
+ * window [support], .h:204-208 (impl .cpp:385-427, 1305-1326). */
+void sdp_gridder_make_kernel(
+        const sdp_Mem* window,
+        sdp_Mem* kernel,
+        sdp_Error* status
+);
+
+/* PSWF kernel [oversampling + 1, support], .h:221-225 (.cpp:1329-1350). */
+void sdp_gridder_make_pswf_kernel(
+        int support,
+        sdp_Mem* kernel,
+        sdp_Error* status
+);
+
+/* exp(2 pi i w_step n(l, m)) [subgrid_size, subgrid_size] complex double,
+ * .h:240-248 (.cpp:1353-1380). */
+void sdp_gridder_make_w_pattern(
+        int subgrid_size,
+        double theta,
+        double shear_u,
+        double shear_v,
+        double w_step,
+        sdp_Mem* w_pattern,
+        sdp_Error* status
+);
+
+/* sqrt(mean(|a - b|^2)), .h:276-280 (.cpp:1469-1538). */
+double sdp_gridder_rms_diff(
+        const sdp_Mem* a,
+        const sdp_Mem* b,
+        sdp_Error* status
+);
+
+/* out = in1 / in2 ** exponent, .h:296-302 (.cpp:1541-1667). */
+void sdp_gridder_scale_inv_array(
+        sdp_Mem* out,
+        const sdp_Mem* in1,
+        const sdp_Mem* in2,
+        int exponent,
+        sdp_Error* status
+);
+
+/* subgrids[:-1] = subgrids[1:], .h:310 (.cpp:1670-1726). */
+void sdp_gridder_shift_subgrids(sdp_Mem* subgrids, sdp_Error* status);
+
+/* grid (periodically wrapped) += factor * subgrid at -offset,
+ * .h:322-329 (.cpp:553-601, 1729-1822). */
+void sdp_gridder_subgrid_add(
+        sdp_Mem* grid,
+        int offset_u,
+        int offset_v,
+        const sdp_Mem* subgrid,
+        double factor,
+        sdp_Error* status
+);
+
+/* subgrid = grid at offset (periodic), .h:340-346 (.cpp:603-649). */
+void sdp_gridder_subgrid_cut_out(
+        const sdp_Mem* grid,
+        int offset_u,
+        int offset_v,
+        sdp_Mem* subgrid,
+        sdp_Error* status
+);
+
+/* result = sum(a[start:end] - b[start:end]), int32 arrays; start < 0 or
+ * end < 0: all rows. .h:358-365 (.cpp:652-679, 1919-1989). */
+void sdp_gridder_sum_diff(
+        const sdp_Mem* a,
+        const sdp_Mem* b,
+        int64_t* result,
+        int64_t start_row,
+        int64_t end_row,
+        sdp_Error* status
+);
+
+/* Scaled uvw bounding box of the selected channels, starting from 0 in
+ * every dimension, .h:379-388 (.cpp:682-719, 1992-2102). */
+void sdp_gridder_uvw_bounds_all(
+        const sdp_Mem* uvws,
+        double freq0_hz,
+        double dfreq_hz,
+        const sdp_Mem* start_chs,
+        const sdp_Mem* end_chs,
+        double uvw_min[3],
+        double uvw_max[3],
+        sdp_Error* status
+);
+
+/* Channel ranges restricted to min_u <= u < max_u in dimension dim,
+ * sdp_gridder_clamp_channels.h:42-56 (impl clamp_channels.cpp). */
+void sdp_gridder_clamp_channels_single(
+        const sdp_Mem* uvws,
+        const int dim,
+        const double freq0_hz,
+        const double dfreq_hz,
+        const sdp_Mem* start_ch_in,
+        const sdp_Mem* end_ch_in,
+        const double min_u,
+        const double max_u,
+        sdp_Mem* start_ch_out,
+        sdp_Mem* end_ch_out,
+        int64_t start_row,
+        int64_t end_row,
+        sdp_Error* status
+);
+
+/* Same in u and v, sdp_gridder_clamp_channels.h:72-87. */
+void sdp_gridder_clamp_channels_uv(
+        const sdp_Mem* uvws,
+        const double freq0_hz,
+        const double dfreq_hz,
+        const sdp_Mem* start_ch_in,
+        const sdp_Mem* end_ch_in,
+        const double min_u,
+        const double max_u,
+        const double min_v,
+        const double max_v,
+        sdp_Mem* start_ch_out,
+        sdp_Mem* end_ch_out,
+        int64_t start_row,
+        int64_t end_row,
+        sdp_Error* status
+);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,578 @@
+"""TEST INFRASTRUCTURE ONLY -- numpy oracle for the w-towers gridder.
+
+A restatement (float64 / complex128 throughout) of ska-sdp-func 1.2.2:
+  sdp_gridder_wtower_uvw.cpp    create :660-723, degrid :726-909 (kernel
+                                :45-176), grid :935-1123 (kernel :352-484),
+                                grid_correct / degrid_correct :912-932,
+                                :1126-1146
+  sdp_gridder_utils.cpp         make_kernel :385-427, make_pswf_kernel
+                                :1329-1350, make_w_pattern :1353-1380,
+                                scale_inv_array :487-526, shift_subgrids
+                                :529-550, subgrid_add / cut_out :553-649,
+                                uvw_bounds_all :682-719, determine_w_step
+                                :1016-1039
+  sdp_gridder_utils.h           lm_to_n :399-412
+  sdp_gridder_clamp_channels.h  clamp_channels_inline :86-146
+  sdp_gridder_grid_correct.cpp  grid_corr_pswf :18-77, grid_corr_w_stack
+                                :81-116
+  sdp_pswf.cpp                  generate_pswf :570-601 (values of the
+                                prolate spheroidal angular function S_00,
+                                here from scipy.special.pro_ang1, the same
+                                Zhang & Jin algorithm the reference ports)
+  sdp_fft.cpp                   unnormalised C2C, fft_phase :1047-1062
+  sdp_grid_wstack_wtower.cpp    grid_all :467-700, degrid_all :218-448
+Used only by tests/ as the checker of the HIP implementation.
+
+Parity status: the reference's CPU path could not be run here (DESIGN.md,
+"Denied"); absolute values are pinned by the DFT (the gridder must reproduce
+a direct Fourier sum to its kernel accuracy) and the PSWF values by scipy.
+"""
+import math
+
+import numpy as np
+import scipy.special
+
+C_0 = 299792458.0
+
+
+# -- kernels --------------------------------------------------------------
+
+def pswf_values(c, x):
+    """S_00(c, x) (Flammer normalisation, S(0) = 1) for |x| < 1."""
+    x = np.atleast_1d(np.asarray(x, np.float64))
+    return np.array([scipy.special.pro_ang1(0, 0, c, float(v))[0] for v in x])
+
+
+def generate_pswf(c, size, end_correction=False):
+    """sdp_pswf.cpp:570-601."""
+    out = np.zeros(size)
+    out[size // 2] = pswf_values(c, 0.0)[0]
+    i = np.arange(1, size // 2)
+    if len(i):
+        v = pswf_values(c, 2.0 * i / size)
+        out[size // 2 + i] = v
+        out[size // 2 - i] = v
+    if end_correction and size % 2 == 0:
+        out[0] = 1e-15
+    return out
+
+
+def make_kernel(window, oversampling):
+    """Oversampled uv kernel from an image-space window, utils.cpp:385-427."""
+    support = len(window)
+    half = support // 2
+    i = np.arange(oversampling + 1)[:, None]
+    s_out = np.arange(support)[None, :]
+    du = (i - oversampling).astype(np.float64)
+    u = (s_out - half) - du / oversampling
+    l = (np.arange(support) - half) / support
+    val = np.einsum("k,abk->ab", window,
+                    np.cos(2 * np.pi * u[:, :, None] * l[None, None, :]))
+    return val / support
+
+
+def make_pswf_kernel(support, oversampling):
+    """utils.cpp:1329-1350."""
+    pswf = generate_pswf(support * (np.pi / 2), support)
+    if support % 2 == 0:
+        pswf[0] = 1e-15
+    return make_kernel(pswf, oversampling)
+
+
+def lm_to_n(l, m, h_u, h_v):
+    """utils.h:399-412."""
+    if h_u == 0 and h_v == 0:
+        return np.sqrt(1 - l * l - m * m) - 1
+    a = h_u * l + h_v * m - 1
+    b = h_u * h_u + h_v * h_v + 1
+    return (np.sqrt(a * a - b * (l * l + m * m)) + a) / b
+
+
+def make_w_pattern(subgrid_size, theta, shear_u, shear_v, w_step):
+    """utils.cpp:1353-1380."""
+    half = subgrid_size // 2
+    il = np.arange(subgrid_size)
+    l = (il - half) * theta / subgrid_size
+    n = lm_to_n(l[:, None], l[None, :], shear_u, shear_v)
+    phase = 2.0 * np.pi * w_step * n
+    return np.cos(phase) + 1j * np.sin(phase)
+
+
+def determine_w_step(theta, fov, shear_u, shear_v, x0=0.0):
+    """utils.cpp:1016-1039."""
+    if x0 == 0.0:
+        x0 = fov / theta
+    v = [lm_to_n(a, b, shear_u, shear_v)
+         for a, b in ((-fov / 2, -fov / 2), (fov / 2, -fov / 2),
+                      (-fov / 2, fov / 2), (fov / 2, fov / 2))]
+    fov_n = 2.0 * -min(min(v[0], v[1]), min(v[2], v[3]))
+    return 1.0 / (fov_n / x0)
+
+
+# -- helpers ----------------------------------------------------------------
+
+def fft_phase(a):
+    """(-1)^(i+j), sdp_fft.cpp:1047-1062."""
+    i = np.arange(a.shape[0])[:, None]
+    j = np.arange(a.shape[1])[None, :]
+    return a * (1 - (((i + j) & 1) << 1))
+
+
+def fft_shift(a, forward):
+    """phase * FFT * phase, unnormalised (sdp_fft_exec_shift without norm)."""
+    a = fft_phase(a)
+    if forward:
+        a = np.fft.fft2(a)
+    else:
+        a = np.fft.ifft2(a) * (a.shape[0] * a.shape[1])
+    return fft_phase(a)
+
+
+def clamp_channels(u, f0, df, start_ch, end_ch, min_u, max_u):
+    """clamp_channels.h:86-146 (scalar)."""
+    u0 = f0 * u / C_0
+    du = df * u / C_0
+    eta = max(abs(min_u - u0), abs(max_u - u0)) / 2147483645.0
+    if du > eta:
+        start_ch = max(start_ch, int(math.ceil((min_u - u0) / du)))
+        end_ch = min(end_ch, int(math.ceil((max_u - u0) / du)))
+    elif du < -eta:
+        start_ch = max(start_ch, int(math.ceil((max_u - u0) / du)))
+        end_ch = min(end_ch, int(math.ceil((min_u - u0) / du)))
+    else:
+        if min_u > u0 or max_u <= u0:
+            start_ch, end_ch = 0, 0
+    if end_ch <= start_ch:
+        start_ch, end_ch = 0, 0
+    return start_ch, end_ch
+
+
+def clamp_channels_vec(u, f0, df, start_ch, end_ch, min_u, max_u):
+    """clamp_channels over arrays of rows (same arithmetic, vectorised)."""
+    u = np.asarray(u, np.float64)
+    s = np.array(start_ch, np.int64)
+    e = np.array(end_ch, np.int64)
+    u0 = f0 * u / C_0
+    du = df * u / C_0
+    eta = np.maximum(np.abs(min_u - u0), np.abs(max_u - u0)) / 2147483645.0
+    with np.errstate(divide="ignore", invalid="ignore"):
+        a = np.ceil((min_u - u0) / du)
+        b = np.ceil((max_u - u0) / du)
+    pos = du > eta
+    neg = du < -eta
+    mid = ~pos & ~neg
+    s = np.where(pos, np.maximum(s, np.where(pos, a, 0).astype(np.int64)), s)
+    e = np.where(pos, np.minimum(e, np.where(pos, b, 0).astype(np.int64)), e)
+    s = np.where(neg, np.maximum(s, np.where(neg, b, 0).astype(np.int64)), s)
+    e = np.where(neg, np.minimum(e, np.where(neg, a, 0).astype(np.int64)), e)
+    out = mid & ((min_u > u0) | (max_u <= u0))
+    s = np.where(out, 0, s)
+    e = np.where(out, 0, e)
+    empty = e <= s
+    return np.where(empty, 0, s), np.where(empty, 0, e)
+
+
+def uvw_bounds_all(uvws, f0, df, start_chs, end_chs):
+    """utils.cpp:682-719, 1992-2011 (bounds start at +/-inf)."""
+    lo = [math.inf, math.inf, math.inf]
+    hi = [-math.inf, -math.inf, -math.inf]
+    for i in range(uvws.shape[0]):
+        s, e = int(start_chs[i]), int(end_chs[i])
+        if s >= e:
+            continue
+        for j in range(3):
+            u0 = f0 * float(uvws[i, j]) / C_0
+            du = df * float(uvws[i, j]) / C_0
+            if uvws[i, j] >= 0:
+                lo[j] = min(u0 + s * du, lo[j])
+                hi[j] = max(u0 + (e - 1) * du, hi[j])
+            else:
+                hi[j] = max(u0 + s * du, hi[j])
+                lo[j] = min(u0 + (e - 1) * du, lo[j])
+    return lo, hi
+
+
+def subgrid_add(grid, offset_u, offset_v, subgrid, factor):
+    """utils.cpp:553-601 (periodic wrap)."""
+    su, sv = subgrid.shape
+    gu, gv = grid.shape
+    i1 = (np.arange(su) + gu // 2 - su // 2 - offset_u) % gu
+    j1 = (np.arange(sv) + gv // 2 - sv // 2 - offset_v) % gv
+    grid[np.ix_(i1, j1)] += subgrid * factor
+
+
+def subgrid_cut_out(grid, offset_u, offset_v, su, sv):
+    """utils.cpp:603-649."""
+    gu, gv = grid.shape
+    i1 = (np.arange(su) + gu // 2 - su // 2 + offset_u) % gu
+    j1 = (np.arange(sv) + gv // 2 - sv // 2 + offset_v) % gv
+    return grid[np.ix_(i1, j1)].copy()
+
+
+# -- the sub-grid gridder -----------------------------------------------------
+
+class WtowerPlan:
+    """sdp_GridderWtowerUVW (create: wtower_uvw.cpp:660-723)."""
+
+    def __init__(self, image_size, subgrid_size, theta, w_step, shear_u,
+                 shear_v, support, oversampling, w_support, w_oversampling):
+        assert subgrid_size % 2 == 0
+        self.image_size = image_size
+        self.subgrid_size = subgrid_size
+        self.theta = theta
+        self.w_step = w_step
+        self.shear_u = shear_u
+        self.shear_v = shear_v
+        self.support = support
+        self.oversampling = oversampling
+        self.w_support = w_support
+        self.w_oversampling = w_oversampling
+        self.uv_kernel = make_pswf_kernel(support, oversampling)
+        self.w_kernel = make_pswf_kernel(w_support, w_oversampling)
+        self.w_pattern = make_w_pattern(subgrid_size, theta, shear_u,
+                                        shear_v, w_step)
+        self.num_w_planes = [0, 0]
+
+    # Visibility selection + kernel offsets for one w-plane, vectorised over
+    # the (row, channel) pairs the reference's loops visit (:80-140).
+    def _select(self, w_plane, off_u, off_v, off_w, f0, df, uvws,
+                start_chs, end_chs, start_row, end_row):
+        half = self.subgrid_size // 2
+        os_, wos = self.oversampling, self.w_oversampling
+        sup = self.support
+        theta, w_step = self.theta, self.w_step
+        theta_ov = theta * os_
+        w_step_ov = 1.0 / w_step * wos
+        half_ov = (half - sup // 2 + 1) * os_
+        r = np.arange(start_row, end_row)
+        s = start_chs[start_row:end_row].astype(np.int64)
+        e = end_chs[start_row:end_row].astype(np.int64)
+        uvw_r = uvws[start_row:end_row].astype(np.float64)
+        min_w = (w_plane + off_w - 1) * w_step
+        max_w = (w_plane + off_w) * w_step
+        live = s < e
+        s, e = clamp_channels_vec(uvw_r[:, 2], f0, df, s, e, min_w, max_w)
+        live &= s < e
+        s0, sd = f0 / C_0, df / C_0
+        u0 = uvw_r[:, 0] * s0 - off_u / theta
+        v0 = uvw_r[:, 1] * s0 - off_v / theta
+        du, dv = uvw_r[:, 0] * sd, uvw_r[:, 1] * sd
+        umin = np.floor(theta * (u0 + s * du))
+        umax = np.ceil(theta * (u0 + (e - 1) * du))
+        vmin = np.floor(theta * (v0 + s * dv))
+        vmax = np.ceil(theta * (v0 + (e - 1) * dv))
+        live &= ~((umin < -half) | (umax >= half) | (vmin < -half)
+                  | (vmax >= half))
+        r, s, e = r[live], s[live], e[live]
+        counts = e - s
+        rows = np.repeat(r, counts).astype(np.int64)
+        chans = (np.arange(counts.sum()) - np.repeat(np.cumsum(counts)
+                                                     - counts, counts)
+                 + np.repeat(s, counts)).astype(np.int64)
+        if len(rows) == 0:
+            return rows, chans, None
+        uvw = uvws[rows].astype(np.float64)
+        s0, sd = f0 / C_0, df / C_0
+        u = uvw[:, 0] * s0 - off_u / theta + chans * (uvw[:, 0] * sd)
+        v = uvw[:, 1] * s0 - off_v / theta + chans * (uvw[:, 1] * sd)
+        w = (uvw[:, 2] * s0 - (off_w + w_plane - 1) * w_step
+             + chans * (uvw[:, 2] * sd))
+        # C++ int(round(x)): round half away from zero, truncate to int.
+        iu0_ov = (np.sign(u * theta_ov) * np.floor(np.abs(u * theta_ov) + 0.5)
+                  ).astype(np.int64) + half_ov
+        iv0_ov = (np.sign(v * theta_ov) * np.floor(np.abs(v * theta_ov) + 0.5)
+                  ).astype(np.int64) + half_ov
+        iw0_ov = (np.sign(w * w_step_ov)
+                  * np.floor(np.abs(w * w_step_ov) + 0.5)).astype(np.int64)
+        # A negative oversampled index would read the kernel tables before
+        # their start in the reference (undefined); such visibilities are
+        # skipped, as by the HIP kernels.
+        ok = (iu0_ov >= 0) & (iv0_ov >= 0) & (iw0_ov >= 0)
+        rows, chans = rows[ok], chans[ok]
+        iu0_ov, iv0_ov, iw0_ov = iu0_ov[ok], iv0_ov[ok], iw0_ov[ok]
+        if len(rows) == 0:
+            return rows, chans, None
+        idx = dict(iu0=iu0_ov // os_, iv0=iv0_ov // os_,
+                   u_off=(iu0_ov % os_), v_off=(iv0_ov % os_),
+                   w_off=iw0_ov % wos)
+        return rows, chans, idx
+
+    def _flat_cells(self, idx):
+        """Flat indices into the [w_support, S, S] stack of every tap, as the
+        reference's contiguous indexing computes them (taps past a layer's
+        edge land in the neighbouring layer); -1 outside the stack."""
+        S, wsup, sup = self.subgrid_size, self.w_support, self.support
+        iw = np.arange(wsup)[None, :, None, None]
+        iu = (idx["iu0"][:, None] + np.arange(sup)[None, :])[:, None, :, None]
+        iv = (idx["iv0"][:, None] + np.arange(sup)[None, :])[:, None, None, :]
+        f = (iw * S + iu) * S + iv                       # (n, w, u, v)
+        return np.where((f >= 0) & (f < wsup * S * S), f, -1)
+
+    def _w_range(self, uvws, f0, df, start_chs, end_chs, off_w):
+        lo, hi = uvw_bounds_all(uvws, f0, df, start_chs, end_chs)
+        if not lo[2] <= hi[2]:
+            return None
+        eta = 1e-5
+        first = int(math.floor(lo[2] / self.w_step - eta)) - off_w
+        last = int(math.ceil(hi[2] / self.w_step + eta)) - off_w + 1
+        return first, last
+
+    def _taps(self, idx):
+        sup, wsup = self.support, self.w_support
+        ku = self.uv_kernel[idx["u_off"]]          # (n, sup)
+        kv = self.uv_kernel[idx["v_off"]]
+        kw = self.w_kernel[idx["w_off"]]           # (n, wsup)
+        return ku, kv, kw
+
+    def degrid(self, subgrid_image, off_u, off_v, off_w, f0, df, uvws,
+               start_chs, end_chs, vis, start_row=-1, end_row=-1):
+        """wtower_uvw.cpp:726-909; vis += (in place)."""
+        if df == 0.0:
+            df = 10
+        if start_row < 0 or end_row < 0:
+            start_row, end_row = 0, uvws.shape[0]
+        S, wsup, sup = self.subgrid_size, self.w_support, self.support
+        rng = self._w_range(uvws, f0, df, start_chs, end_chs, off_w)
+        if rng is None:
+            return vis
+        first, last = rng
+        wimg = subgrid_image.astype(np.complex128) / self.w_pattern ** (
+            first - wsup // 2)
+        stack = np.zeros((wsup, S, S), np.complex128)
+        for i in range(wsup):
+            stack[i] = fft_shift(wimg, True)
+            wimg = wimg / self.w_pattern
+        for w_plane in range(first, last + 1):
+            if w_plane != first:
+                stack[:-1] = stack[1:].copy()
+                stack[-1] = fft_shift(wimg, True)
+                wimg = wimg / self.w_pattern
+            rows, chans, idx = self._select(w_plane, off_u, off_v, off_w, f0,
+                                            df, uvws, start_chs, end_chs,
+                                            start_row, end_row)
+            if idx is None:
+                continue
+            ku, kv, kw = self._taps(idx)
+            f = self._flat_cells(idx)
+            flat = np.append(stack.ravel(), 0)       # index -1 reads 0
+            sub = flat[f]                            # (n, w, u, v)
+            val = np.einsum("nwuv,nu,nv,nw->n", sub, ku, kv, kw)
+            np.add.at(vis, (rows, chans), val.astype(vis.dtype))
+        self.num_w_planes[0] += 1 + last - first
+        return vis
+
+    def grid(self, vis, uvws, start_chs, end_chs, f0, df, subgrid_image,
+             off_u, off_v, off_w, start_row=-1, end_row=-1):
+        """wtower_uvw.cpp:935-1123; subgrid_image += (in place)."""
+        if df == 0.0:
+            df = 10
+        if start_row < 0 or end_row < 0:
+            start_row, end_row = 0, uvws.shape[0]
+        S, wsup, sup = self.subgrid_size, self.w_support, self.support
+        rng = self._w_range(uvws, f0, df, start_chs, end_chs, off_w)
+        if rng is None:
+            return subgrid_image
+        first, last = rng
+        wimg = np.zeros((S, S), np.complex128)
+        stack = np.zeros((wsup, S, S), np.complex128)
+        for w_plane in range(first, last + 1):
+            if w_plane != first:
+                wimg = wimg / self.w_pattern
+                wimg = wimg + fft_shift(stack[0], False)
+                stack[:-1] = stack[1:].copy()
+                stack[-1] = 0
+            rows, chans, idx = self._select(w_plane, off_u, off_v, off_w, f0,
+                                            df, uvws, start_chs, end_chs,
+                                            start_row, end_row)
+            if idx is None:
+                continue
+            ku, kv, kw = self._taps(idx)
+            val = vis[rows, chans].astype(np.complex128)
+            contrib = np.einsum("n,nw,nu,nv->nwuv", val, kw, ku, kv)
+            f = self._flat_cells(idx)
+            keep = f >= 0
+            flat = stack.reshape(-1)
+            np.add.at(flat, f[keep], contrib[keep])
+        for i in range(wsup):
+            wimg = wimg / self.w_pattern
+            wimg = wimg + fft_shift(stack[i], False)
+        if np.iscomplexobj(subgrid_image):
+            subgrid_image += (wimg * self.w_pattern ** (last + wsup // 2 - 1)
+                              ).astype(subgrid_image.dtype)
+        else:
+            # accumulate_scaled_arrays with a real output adds the real part
+            # and ignores the w-pattern (utils.cpp:82-101, 813-832).
+            subgrid_image += wimg.real.astype(subgrid_image.dtype)
+        self.num_w_planes[1] += 1 + last - first
+        return subgrid_image
+
+    def _correct(self, facet, off_l, off_m, w_offset, inverse):
+        """grid_correct.cpp:18-116 (pswf, then w-stack phasor if complex)."""
+        N, theta = self.image_size, self.theta
+        pswf_lm = generate_pswf(self.support * (np.pi / 2), N, True)
+        c_n = self.w_support * (np.pi / 2)
+        nl, nm = facet.shape
+        pl = np.arange(nl) - nl // 2 + off_l
+        pm = np.arange(nm) - nm // 2 + off_m
+        l = pl * theta / N
+        m = pm * theta / N
+        n = lm_to_n(l[:, None], m[None, :], self.shear_u, self.shear_v)
+        n_x = np.abs(n * 2.0 * self.w_step)
+        pswf_n = np.ones_like(n_x)
+        if c_n > 0:
+            inside = n_x < 1.0
+            if np.any(inside):
+                pswf_n[inside] = pswf_values(c_n, n_x[inside])
+        scale = 1.0 / (pswf_lm[pl + N // 2][:, None]
+                       * pswf_lm[pm + N // 2][None, :] * pswf_n)
+        out = facet * scale
+        if np.iscomplexobj(facet) and w_offset != 0:
+            phase = 2.0 * np.pi * self.w_step * n * w_offset
+            w = np.cos(phase) + 1j * np.sin(phase)
+            out = out * (w if inverse else 1.0 / w)
+        facet[...] = out.astype(facet.dtype)
+        return facet
+
+    def grid_correct(self, facet, off_l, off_m, w_offset=0):
+        return self._correct(facet, off_l, off_m, w_offset, True)
+
+    def degrid_correct(self, facet, off_l, off_m, w_offset=0):
+        return self._correct(facet, off_l, off_m, w_offset, False)
+
+
+# -- direct Fourier sums (accuracy pin) ------------------------------------
+
+def dft_subgrid_vis(image, theta, shear_u, shear_v, uvw_l):
+    """Visibilities of a sub-grid image centred on the grid centre:
+    V(u, v, w) = sum_lm I(l, m) exp(-2 pi i (u l + v m + w n)), (l, m) on the
+    image-pixel grid (l = (i - N/2) theta / N), n = lm_to_n(l, m)."""
+    N = image.shape[0]
+    l = (np.arange(N) - N // 2) * theta / N
+    L, M = np.meshgrid(l, l, indexing="ij")
+    n = lm_to_n(L, M, shear_u, shear_v)
+    ph = (uvw_l[:, 0, None] * L.ravel()[None, :]
+          + uvw_l[:, 1, None] * M.ravel()[None, :]
+          + uvw_l[:, 2, None] * n.ravel()[None, :])
+    return np.exp(-2j * np.pi * ph) @ image.ravel()
+
+
+# -- array-level helpers of the library ----------------------------------
+
+def clamp_channels_rows(uvws, dim, f0, df, s_in, e_in, min_u, max_u,
+                        start_row=-1, end_row=-1, s_out=None, e_out=None):
+    """sdp_gridder_clamp_channels_single (clamp_channels.cpp:8-62): note
+    u0 = u * (f0 / c), an in-range row with |du| <= eta keeps its input
+    range, and empty ranges become (s, s) rather than (0, 0)."""
+    n = uvws.shape[0]
+    if start_row < 0 or end_row < 0:
+        start_row, end_row = 0, n
+    s_out = np.array(s_in if s_out is None else s_out, np.int64)
+    e_out = np.array(e_in if e_out is None else e_out, np.int64)
+    for i in range(start_row, end_row):
+        u = float(uvws[i, dim])
+        u0 = u * (f0 / C_0)
+        du = u * (df / C_0)
+        eta = max(abs(min_u - u0), abs(max_u - u0)) / 2147483645.0
+        if abs(du) > eta:
+            mins = int(math.ceil((min_u - u0) / du))
+            maxs = int(math.ceil((max_u - u0) / du))
+            a, b = (mins, maxs) if du > 0 else (maxs, mins)
+            s_out[i] = max(int(s_in[i]), a)
+            e_out[i] = min(int(e_in[i]), b)
+        elif min_u > u0 or max_u <= u0:
+            s_out[i], e_out[i] = 0, 0
+        else:
+            s_out[i], e_out[i] = s_in[i], e_in[i]
+        e_out[i] = max(e_out[i], s_out[i])
+    return s_out, e_out
+
+
+def clamp_channels_uv_rows(uvws, f0, df, s_in, e_in, min_u, max_u, min_v,
+                           max_v, start_row=-1, end_row=-1):
+    """sdp_gridder_clamp_channels_uv (clamp_channels.cpp:64-150)."""
+    s, e = clamp_channels_rows(uvws, 0, f0, df, s_in, e_in, min_u, max_u,
+                               start_row, end_row)
+    n = uvws.shape[0]
+    if start_row < 0 or end_row < 0:
+        start_row, end_row = 0, n
+    rows = [i for i in range(start_row, end_row) if s[i] < e[i]]
+    s2, e2 = clamp_channels_rows(uvws, 1, f0, df, s, e, min_v, max_v)
+    out_s, out_e = s.copy(), e.copy()
+    out_s[rows], out_e[rows] = s2[rows], e2[rows]
+    return out_s, out_e
+
+
+def worst_case_sources(image_size, theta, fov):
+    """sdp_gridder_worst_case_image (wtower_height.cpp:272-316)."""
+    fov_edge = int(image_size / theta * fov / 2)
+    while image_size % fov_edge == 0:
+        fov_edge -= 1
+    c = image_size // 2
+    return [(c + fov_edge, c + fov_edge, 0.3), (c - fov_edge, c - fov_edge, 0.2),
+            (c + fov_edge, c - fov_edge - 1, 0.3),
+            (c - fov_edge - 1, c + fov_edge, 0.2)]
+
+
+def gridder_accuracy(plan, fov, subgrid_frac, num_samples, w):
+    """find_gridder_accuracy (wtower_height.cpp:16-184)."""
+    N, S, theta = plan.image_size, plan.subgrid_size, plan.theta
+    if num_samples == 0:
+        num_samples = 3
+    src = sorted(worst_case_sources(N, theta, fov))
+    image = np.zeros((N, N), complex)
+    for il, im, f in src:
+        image[il, im] = f
+    plan.degrid_correct(image, 0, 0)
+    grid = fft_shift(image, True)
+    sub = subgrid_cut_out(grid, 0, 0, S, S)
+    sub = fft_shift(sub, False) / (S * S)
+    if subgrid_frac == 0.0:
+        subgrid_frac = 2.0 / 3.0
+    start = -S * subgrid_frac / theta / 2
+    end = S * subgrid_frac / theta / 2
+    step = (end - start) / (num_samples - 1)
+    uvw = np.array([(start + j * step, start + i * step, w)
+                    for i in range(num_samples) for j in range(num_samples)])
+    R = len(uvw)
+    vis = plan.degrid(sub, 0, 0, 0, C_0, C_0, uvw, np.zeros(R, np.int32),
+                      np.ones(R, np.int32), np.zeros((R, 1), complex))
+    ref = np.zeros(R, complex)
+    for il, im, f in src:
+        l = (il - N // 2) * theta / N
+        m = (im - N // 2) * theta / N
+        n = lm_to_n(l, m, plan.shear_u, plan.shear_v)
+        ref += f * np.exp(-2j * np.pi * (uvw[:, 0] * l + uvw[:, 1] * m
+                                         + uvw[:, 2] * n))
+    return float(np.sqrt(np.mean(np.abs(vis[:, 0] - ref) ** 2)))
+
+
+def determine_max_w_tower_height(image_size, subgrid_size, theta, w_step,
+                                 shear_u, shear_v, support, oversampling,
+                                 w_support, w_oversampling, fov,
+                                 subgrid_frac=0.0, num_samples=0,
+                                 target_err=0.0):
+    """wtower_height.cpp:187-269 (exponential, then binary search)."""
+    plan = WtowerPlan(image_size, subgrid_size, theta, w_step, shear_u,
+                      shear_v, support, oversampling, w_support,
+                      w_oversampling)
+    if target_err == 0.0:
+        target_err = 2 * gridder_accuracy(plan, fov, subgrid_frac,
+                                          num_samples, 0.0)
+    iw, diw, accelerate = 1, 1, True
+    while True:
+        err = gridder_accuracy(plan, fov, subgrid_frac, num_samples,
+                               iw * w_step)
+        if err < target_err:
+            if accelerate:
+                diw *= 2
+            elif diw > 1:
+                diw //= 2
+            else:
+                return 2.0 * iw
+            iw += diw
+        elif diw > 1:
+            diw //= 2
+            iw -= diw
+            accelerate = False
+        else:
+            return 2.0 * (iw - 1)

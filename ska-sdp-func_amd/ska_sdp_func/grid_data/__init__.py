@@ -1,5 +1,35 @@
 """Gridding functions (reference: src/ska_sdp_func/grid_data/__init__.py)."""
 
+from .gridder_utils import (
+    clamp_channels_single,
+    clamp_channels_uv,
+    determine_max_w_tower_height,
+    determine_w_step,
+    find_max_w_tower_height,
+    make_kernel,
+    make_pswf_kernel,
+    make_w_pattern,
+    rms_diff,
+    subgrid_add,
+    subgrid_cut_out,
+    uvw_bounds_all,
+)
 from .gridder_uvw_es_fft import GridderUvwEsFft
+from .gridder_wtower_uvw import GridderWtowerUVW
 
-__all__ = ["GridderUvwEsFft"]
+__all__ = [
+    "GridderUvwEsFft",
+    "GridderWtowerUVW",
+    "clamp_channels_single",
+    "clamp_channels_uv",
+    "determine_max_w_tower_height",
+    "determine_w_step",
+    "find_max_w_tower_height",
+    "make_kernel",
+    "make_pswf_kernel",
+    "make_w_pattern",
+    "rms_diff",
+    "subgrid_add",
+    "subgrid_cut_out",
+    "uvw_bounds_all",
+]
