@@ -576,3 +576,138 @@ def determine_max_w_tower_height(image_size, subgrid_size, theta, w_step,
             accelerate = False
         else:
             return 2.0 * (iw - 1)
+
+
+# -- w-stacking x w-towers driver (sdp_grid_wstack_wtower.cpp) ------------
+
+def clamp_rows_vec(x, f0, df, s_in, e_in, lo, hi):
+    """clamp_channels.cpp:37-62 over arrays of rows (vectorised)."""
+    x = np.asarray(x, np.float64)
+    s_in = np.asarray(s_in, np.int64)
+    e_in = np.asarray(e_in, np.int64)
+    x0 = x * (f0 / C_0)
+    dx = x * (df / C_0)
+    eta = np.maximum(np.abs(lo - x0), np.abs(hi - x0)) / 2147483645.0
+    big = np.abs(dx) > eta
+    with np.errstate(divide="ignore", invalid="ignore"):
+        mins = np.where(big, np.ceil((lo - x0) / np.where(big, dx, 1.0)), 0)
+        maxs = np.where(big, np.ceil((hi - x0) / np.where(big, dx, 1.0)), 0)
+    mins = mins.astype(np.int64)
+    maxs = maxs.astype(np.int64)
+    pos = dx > 0
+    s = np.where(big, np.maximum(s_in, np.where(pos, mins, maxs)), s_in)
+    e = np.where(big, np.minimum(e_in, np.where(pos, maxs, mins)), e_in)
+    out = ~big & ((lo > x0) | (hi <= x0))
+    s = np.where(out, 0, s)
+    e = np.where(out, 0, e)
+    return s, np.maximum(e, s)
+
+
+def _wstack_geometry(uvw, f0, df, num_chan, S, theta, w_step, frac, H):
+    R = uvw.shape[0]
+    if frac == 0.0:
+        frac = 2.0 / 3.0
+    eff = int(math.floor(S * frac))
+    eff_dist = eff / theta
+    ws_dist = H * w_step
+    lo, hi = uvw_bounds_all(uvw, f0, df, np.zeros(R, np.int64),
+                            np.full(R, num_chan, np.int64))
+    eta = 1e-5
+    rng = lambda a, b, d: (int(math.floor(a / d + 0.5 - eta)),
+                           int(math.floor(b / d + 0.5 + eta)))
+    return (eff, eff_dist, ws_dist, rng(lo[0], hi[0], eff_dist),
+            rng(lo[1], hi[1], eff_dist), rng(lo[2], hi[2], ws_dist))
+
+
+def _uv_clamp(uvw, f0, df, sw, ew, iu, iv, eff_dist):
+    min_u = iu * eff_dist - eff_dist / 2
+    max_u = (iu + 1) * eff_dist - eff_dist / 2
+    min_v = iv * eff_dist - eff_dist / 2
+    max_v = (iv + 1) * eff_dist - eff_dist / 2
+    su, eu = clamp_rows_vec(uvw[:, 0], f0, df, sw, ew, min_u, max_u)
+    live = su < eu
+    sv, ev = clamp_rows_vec(uvw[:, 1], f0, df, su, eu, min_v, max_v)
+    return np.where(live, sv, su), np.where(live, ev, eu)
+
+
+def wstack_grid_all(vis, f0, df, uvw, S, theta, w_step, shear_u, shear_v,
+                    support, oversampling, w_support, w_oversampling,
+                    subgrid_frac, w_tower_height, image, plane_offset=0,
+                    plane_stride=1):
+    """sdp_grid_wstack_wtower_grid_all (.cpp:475-736), one thread; image is
+    overwritten. plane_offset / plane_stride select w-stack planes."""
+    N = image.shape[0]
+    plan = WtowerPlan(N, S, theta, w_step, shear_u, shear_v, support,
+                      oversampling, w_support, w_oversampling)
+    R, C = vis.shape
+    eff, eff_dist, ws_dist, (iu0, iu1), (iv0, iv1), (iw0, iw1) = \
+        _wstack_geometry(uvw, f0, df, C, S, theta, w_step, subgrid_frac,
+                         w_tower_height)
+    sg_factor = (N / S) ** 2
+    image[...] = 0
+    s0 = np.zeros(R, np.int64)
+    e0 = np.full(R, C, np.int64)
+    for iw in range(iw0, iw1 + 1):
+        if (iw - iw0) % plane_stride != plane_offset:
+            continue
+        sw, ew = clamp_rows_vec(uvw[:, 2], f0, df, s0, e0,
+                                iw * ws_dist - ws_dist / 2,
+                                (iw + 1) * ws_dist - ws_dist / 2)
+        if np.sum(ew - sw) == 0:
+            continue
+        off_w = int(iw * w_tower_height)
+        grid = np.zeros((N, N), complex)
+        for iu in range(iu0, iu1 + 1):
+            for iv in range(iv0, iv1 + 1):
+                su, eu = _uv_clamp(uvw, f0, df, sw, ew, iu, iv, eff_dist)
+                if np.sum(eu - su) == 0:
+                    continue
+                sub = np.zeros((S, S), complex)
+                plan.grid(vis, uvw, su, eu, f0, df, sub, iu * eff, iv * eff,
+                          off_w)
+                subgrid_add(grid, -iu * eff, -iv * eff, fft_shift(sub, True),
+                            sg_factor)
+        grid = fft_shift(grid, False) / (N * N)
+        plan.grid_correct(grid, 0, 0, off_w)
+        image += grid if np.iscomplexobj(image) else grid.real
+    return image
+
+
+def wstack_degrid_all(image, f0, df, uvw, S, theta, w_step, shear_u,
+                      shear_v, support, oversampling, w_support,
+                      w_oversampling, subgrid_frac, w_tower_height, vis,
+                      plane_offset=0, plane_stride=1):
+    """sdp_grid_wstack_wtower_degrid_all (.cpp:218-472), one thread; vis is
+    overwritten."""
+    N = image.shape[0]
+    plan = WtowerPlan(N, S, theta, w_step, shear_u, shear_v, support,
+                      oversampling, w_support, w_oversampling)
+    R, C = vis.shape
+    eff, eff_dist, ws_dist, (iu0, iu1), (iv0, iv1), (iw0, iw1) = \
+        _wstack_geometry(uvw, f0, df, C, S, theta, w_step, subgrid_frac,
+                         w_tower_height)
+    vis[...] = 0
+    s0 = np.zeros(R, np.int64)
+    e0 = np.full(R, C, np.int64)
+    for iw in range(iw0, iw1 + 1):
+        if (iw - iw0) % plane_stride != plane_offset:
+            continue
+        sw, ew = clamp_rows_vec(uvw[:, 2], f0, df, s0, e0,
+                                iw * ws_dist - ws_dist / 2,
+                                (iw + 1) * ws_dist - ws_dist / 2)
+        if np.sum(ew - sw) == 0:
+            continue
+        off_w = int(iw * w_tower_height)
+        grid = image.astype(complex)
+        plan.degrid_correct(grid, 0, 0, off_w)
+        grid = fft_shift(grid, True)
+        for iu in range(iu0, iu1 + 1):
+            for iv in range(iv0, iv1 + 1):
+                su, eu = _uv_clamp(uvw, f0, df, sw, ew, iu, iv, eff_dist)
+                if np.sum(eu - su) == 0:
+                    continue
+                sub = subgrid_cut_out(grid, iu * eff, iv * eff, S, S)
+                sub = fft_shift(sub, False) / (S * S)
+                plan.degrid(sub, iu * eff, iv * eff, off_w, f0, df, uvw, su,
+                            eu, vis)
+    return vis

@@ -15,6 +15,9 @@ struct Plan2D;
 
 // n_slow x n_fast row-major complex array; dbl selects complex128.
 Plan2D* create_2d(int n_slow, int n_fast, bool dbl, sdp_Error* status);
+// `batch` n_slow x n_fast arrays, `distance` elements apart (in place).
+Plan2D* create_2d_batched(int n_slow, int n_fast, bool dbl, size_t batch,
+        size_t distance, sdp_Error* status);
 void exec_2d(Plan2D* plan, void* data, bool forward, hipStream_t stream,
         sdp_Error* status);
 void destroy_2d(Plan2D* plan);

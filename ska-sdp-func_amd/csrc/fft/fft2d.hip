@@ -37,6 +37,13 @@ bool setup(sdp_Error* status)
 
 Plan2D* create_2d(int n_slow, int n_fast, bool dbl, sdp_Error* status)
 {
+    return create_2d_batched(n_slow, n_fast, dbl, 1,
+            (size_t)n_slow * n_fast, status);
+}
+
+Plan2D* create_2d_batched(int n_slow, int n_fast, bool dbl, size_t batch,
+        size_t distance, sdp_Error* status)
+{
     if (*status) return nullptr;
     if (!sdp_hip::device_available())
     {
@@ -49,12 +56,23 @@ Plan2D* create_2d(int n_slow, int n_fast, bool dbl, sdp_Error* status)
     const size_t lengths[2] = {(size_t)n_fast, (size_t)n_slow};
     const rocfft_precision prec =
             dbl ? rocfft_precision_double : rocfft_precision_single;
+    rocfft_plan_description desc = nullptr;
+    if (batch > 1 || distance != (size_t)n_slow * n_fast)
+    {
+        const size_t strides[2] = {1, (size_t)n_fast};
+        rocfft_plan_description_create(&desc);
+        rocfft_plan_description_set_data_layout(desc,
+                rocfft_array_type_complex_interleaved,
+                rocfft_array_type_complex_interleaved, nullptr, nullptr,
+                2, strides, distance, 2, strides, distance);
+    }
     rocfft_status e1 = rocfft_plan_create(&p->forward,
             rocfft_placement_inplace, rocfft_transform_type_complex_forward,
-            prec, 2, lengths, 1, nullptr);
+            prec, 2, lengths, batch, desc);
     rocfft_status e2 = rocfft_plan_create(&p->inverse,
             rocfft_placement_inplace, rocfft_transform_type_complex_inverse,
-            prec, 2, lengths, 1, nullptr);
+            prec, 2, lengths, batch, desc);
+    if (desc) rocfft_plan_description_destroy(desc);
     if (e1 != rocfft_status_success || e2 != rocfft_status_success)
     {
         *status = SDP_ERR_RUNTIME;

@@ -1,0 +1,1551 @@
+// MI355X-native w-stacking x w-towers imaging driver
+// (sdp_grid_wstack_wtower.cpp of ska-sdp-func 1.2.2: degrid_all :218-472,
+// grid_all :475-736).
+//
+// Reference structure: for every w-stack plane iw, channel clamps over all
+// rows select the plane's visibilities; for every sub-grid (iu, iv) a
+// second clamp over all rows selects the sub-grid's visibilities
+// (count_visibilities, O(rows x sub-grids)); sub-grid tasks then run one
+// after the other through sdp_gridder_wtower_uvw_(de)grid, each moving a
+// w_support-deep stack through its own w-layers with one S x S FFT per
+// layer.
+//
+// Here:
+//  1. Binning (k_bin): one pass over the rows evaluates, with the
+//     reference's own clamp arithmetic, which (w-stack plane, sub-grid,
+//     w-layer) every channel run of every row belongs to, including the
+//     sub-grid bounds check of the (de)gridding kernel. Items are sorted by
+//     (plane group, w-layer, sub-grid slot) with a device radix sort.
+//  2. Towers: all sub-grids of a w-stack plane (up to a memory budget per
+//     group) move through the w-layers in lock step. A visibility's
+//     contribution does not depend on where its tower starts or ends (the
+//     w-pattern exponents cancel), so one common layer range
+//     per group replaces the per-task ranges. Per layer: one batched S x S
+//     rocFFT over the group and one fused element-wise pass; the FFT-shift
+//     checkerboards are folded into the neighbouring passes (exact sign
+//     flips).
+//  3. (De)gridding kernels: one wavefront per item, lanes over the uv taps,
+//     looping over the w_support layers (512 taps per visibility at
+//     support 8); gridding adds with device atomics into the stack.
+//  4. Image side per w-stack plane: one gather pass sums the sub-grids into
+//     the full grid in the reference's task order (no atomics, no zeroing),
+//     one G x G rocFFT, one fused pass for normalisation, grid correction
+//     and image accumulation (and the mirror for degridding).
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include <hipcub/hipcub.hpp>
+
+#include "ska-sdp-func/grid_data/sdp_grid_wstack_wtower.h"
+#include "ska-sdp-func/grid_data/sdp_gridder_wtower_uvw.h"
+#include "wtower_dev.h"
+#include "wtower_ops.h"
+#include "wtower_plan.h"
+#include "../fft/fft2d.h"
+#include "../utility/sdp_hip.h"
+
+using namespace sdp_wt;
+
+namespace {
+
+constexpr int kWaves = 4;            // wavefronts per (de)gridding block
+
+// ---------------------------------------------------------------------------
+// Geometry of one call (sdp_grid_wstack_wtower.cpp:297-330 / 567-602).
+struct Geo
+{
+    double f0, df;
+    int64_t num_rows, num_chan;
+    int S, eff, support, w_support;
+    double theta, w_step, H, eff_dist, ws_dist;
+    int64_t min_iu, max_iu, min_iv, max_iv, min_iw, max_iw;
+    int64_t nu, nv, niw, ntask;
+    int64_t P0, NP;                  // global w-layer index base and count
+    int plane_offset, plane_stride;
+};
+
+// sdp_gridder_clamp_channels_single / _uv row arithmetic
+// (sdp_gridder_clamp_channels.cpp:37-62).
+__device__ __forceinline__ void clamp_rows(double x, double f0, double df,
+        int s_in, int e_in, double lo, double hi, int* s_out, int* e_out)
+{
+#pragma clang fp contract(off)
+    const double x0 = x * (f0 / kC0);
+    const double dx = x * (df / kC0);
+    const double eta = fmax(fabs(lo - x0), fabs(hi - x0)) / 2147483645.0;
+    int s, e;
+    if (fabs(dx) > eta)
+    {
+        const int mins = (int)(int64_t)ceil((lo - x0) / dx);
+        const int maxs = (int)(int64_t)ceil((hi - x0) / dx);
+        const bool pos = dx > 0;
+        s = max(s_in, pos ? mins : maxs);
+        e = min(e_in, pos ? maxs : mins);
+    }
+    else if (lo > x0 || hi <= x0)
+    {
+        s = 0;
+        e = 0;
+    }
+    else
+    {
+        s = s_in;
+        e = e_in;
+    }
+    *s_out = s;
+    *e_out = max(e, s);
+}
+
+// Candidate index range of x_c = x (f0 + c df) / c0 over channels [s, e)
+// for cells [i d - d/2, (i+1) d - d/2), one cell of margin on each side.
+__device__ __forceinline__ void cell_range(double x, double f0, double df,
+        int s, int e, double d, int64_t lo_lim, int64_t hi_lim, int64_t* lo,
+        int64_t* hi)
+{
+    const double a = f0 * x / kC0 + s * (df * x / kC0);
+    const double b = f0 * x / kC0 + (e - 1) * (df * x / kC0);
+    const double mn = fmin(a, b), mx = fmax(a, b);
+    *lo = max((int64_t)floor(mn / d + 0.5) - 1, lo_lim);
+    *hi = min((int64_t)floor(mx / d + 0.5) + 1, hi_lim);
+}
+
+// Task slot of (w-stack plane, sub-grid) after host assignment.
+struct Slot
+{
+    int group, slot;
+};
+
+struct BinOut
+{
+    // count pass
+    int64_t* row_count;
+    unsigned char* occupied;         // [niw][ntask]
+    // emit pass
+    const int64_t* row_offset;
+    const Slot* slot_map;            // [niw][ntask]
+    uint64_t* keys;
+    uint32_t* idx;
+    int4* items;                     // row, c0, c1, slot (unsorted)
+    unsigned int* hist;              // [groups][NP]
+    int64_t t_cap;
+};
+
+// One pass over the rows: every channel run of every row that the
+// reference would (de)grid, with its w-stack plane, sub-grid and w-layer.
+template<typename U, bool EMIT>
+__global__ void k_bin(const U* __restrict__ uvw, Geo g, BinOut out)
+{
+#pragma clang fp contract(off)
+    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (r >= g.num_rows) return;
+    const double u = (double)uvw[3 * r];
+    const double v = (double)uvw[3 * r + 1];
+    const double w = (double)uvw[3 * r + 2];
+    const int C = (int)g.num_chan;
+    int64_t pos = EMIT ? out.row_offset[r] : 0;
+    int64_t count = 0;
+    int64_t iw_lo, iw_hi;
+    cell_range(w, g.f0, g.df, 0, C, g.ws_dist, g.min_iw, g.max_iw, &iw_lo,
+            &iw_hi);
+    for (int64_t iw = iw_lo; iw <= iw_hi; ++iw)
+    {
+        const int64_t iw_rel = iw - g.min_iw;
+        if (iw_rel % g.plane_stride != g.plane_offset) continue;
+        // Visibilities on the w-stack plane (.cpp:336-343 / 612-618).
+        const double min_w = iw * g.ws_dist - g.ws_dist / 2;
+        const double max_w = (iw + 1) * g.ws_dist - g.ws_dist / 2;
+        int sw, ew;
+        clamp_rows(w, g.f0, g.df, 0, C, min_w, max_w, &sw, &ew);
+        if (sw >= ew) continue;
+        const int off_w = (int)(iw * g.H);
+        int64_t iu_lo, iu_hi;
+        cell_range(u, g.f0, g.df, sw, ew, g.eff_dist, g.min_iu, g.max_iu,
+                &iu_lo, &iu_hi);
+        for (int64_t iu = iu_lo; iu <= iu_hi; ++iu)
+        {
+            // Sub-grid selection (clamp_channels_uv, .cpp:399-406).
+            const double min_u = iu * g.eff_dist - g.eff_dist / 2;
+            const double max_u = (iu + 1) * g.eff_dist - g.eff_dist / 2;
+            int su, eu;
+            clamp_rows(u, g.f0, g.df, sw, ew, min_u, max_u, &su, &eu);
+            if (su >= eu) continue;
+            int64_t iv_lo, iv_hi;
+            cell_range(v, g.f0, g.df, su, eu, g.eff_dist, g.min_iv, g.max_iv,
+                    &iv_lo, &iv_hi);
+            for (int64_t iv = iv_lo; iv <= iv_hi; ++iv)
+            {
+                const double min_v = iv * g.eff_dist - g.eff_dist / 2;
+                const double max_v = (iv + 1) * g.eff_dist - g.eff_dist / 2;
+                int sv, ev;
+                clamp_rows(v, g.f0, g.df, su, eu, min_v, max_v, &sv, &ev);
+                if (sv >= ev) continue;
+                const int64_t task = (iu - g.min_iu) * g.nv + (iv - g.min_iv);
+                if (!EMIT)
+                    out.occupied[iw_rel * g.ntask + task] = 1;
+                Slot sl = {0, 0};
+                if (EMIT) sl = out.slot_map[iw_rel * g.ntask + task];
+                const int off_u = (int)(iu * g.eff);
+                const int off_v = (int)(iv * g.eff);
+                // w-layers of the tower (sdp_gridder_wtower_uvw.cpp:95-119).
+                const double s_uvw0 = g.f0 / kC0, s_duvw = g.df / kC0;
+                double uvw0[3] = {u * s_uvw0, v * s_uvw0, w * s_uvw0};
+                const double duvw[3] = {u * s_duvw, v * s_duvw, w * s_duvw};
+                uvw0[0] -= off_u / g.theta;
+                uvw0[1] -= off_v / g.theta;
+                const double wa = w * s_uvw0 + sv * duvw[2];
+                const double wb = w * s_uvw0 + (ev - 1) * duvw[2];
+                const int64_t p_lo = (int64_t)floor(fmin(wa, wb) / g.w_step);
+                const int64_t p_hi = (int64_t)floor(fmax(wa, wb) / g.w_step)
+                        + 2;
+                for (int64_t P = p_lo; P <= p_hi; ++P)
+                {
+                    const int64_t w_plane = P - off_w;
+                    int64_t sp = sv, ep = ev;
+                    const double pmin = (w_plane + off_w - 1) * g.w_step;
+                    const double pmax = (w_plane + off_w) * g.w_step;
+                    clamp_inline(w, g.f0, g.df, &sp, &ep, pmin, pmax);
+                    if (sp >= ep) continue;
+                    // Sub-grid bounds check of the (de)gridding kernel.
+                    const int half = g.S / 2;
+                    const double u_min = floor(g.theta * (uvw0[0] +
+                            sp * duvw[0]));
+                    const double u_max = ceil(g.theta * (uvw0[0] +
+                            (ep - 1) * duvw[0]));
+                    const double v_min = floor(g.theta * (uvw0[1] +
+                            sp * duvw[1]));
+                    const double v_max = ceil(g.theta * (uvw0[1] +
+                            (ep - 1) * duvw[1]));
+                    if (u_min < -half || u_max >= half || v_min < -half ||
+                            v_max >= half)
+                        continue;
+                    const int64_t p_rel = P - g.P0;
+                    if (p_rel < 0 || p_rel >= g.NP) continue;  // (never)
+                    if (EMIT)
+                    {
+                        const uint64_t key = ((uint64_t)sl.group * g.NP +
+                                p_rel) * out.t_cap + sl.slot;
+                        out.keys[pos] = key;
+                        out.idx[pos] = (uint32_t)pos;
+                        out.items[pos] = make_int4((int)r, (int)sp, (int)ep,
+                                sl.slot);
+                        atomicAdd(&out.hist[sl.group * g.NP + p_rel], 1u);
+                        ++pos;
+                    }
+                    ++count;
+                }
+            }
+        }
+    }
+    if (!EMIT) out.row_count[r] = count;
+}
+
+// First n entries = a, next n = b.
+__global__ void k_fill_int(int* p, int64_t n, int a, int b)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < 2 * n) p[i] = (i < n) ? a : b;
+}
+
+__global__ void k_gather_items(const uint32_t* __restrict__ idx,
+        const int4* __restrict__ in, int4* __restrict__ out, int64_t n)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[idx[i]];
+}
+
+// ---------------------------------------------------------------------------
+// Per-group parameters of the tower kernels.
+struct TowerParams
+{
+    int S, support, w_support, os, wos;
+    double theta, w_step, f0, df;
+    int64_t num_chan;
+    int off_w, w_plane, ring;
+    int64_t layer;                   // S * S
+    int64_t layer_stride;            // slots_alloc * S * S (layer-major)
+    const int* task;                 // slot -> task id
+    int64_t nv, min_iu, min_iv;
+    int eff;
+};
+
+__device__ __forceinline__ int parity_sign(int64_t a)
+{
+    return (a & 1) ? -1 : 1;
+}
+
+struct Taps2
+{
+    int iu0, iv0, u_off, v_off, w_off;
+    bool valid;
+};
+
+// Kernel offsets of channel c (sdp_gridder_wtower_uvw.cpp:121-141).
+template<typename U>
+__device__ __forceinline__ Taps2 item_taps(const TowerParams& p,
+        const U* __restrict__ uvws, int row, int c, int off_u, int off_v)
+{
+#pragma clang fp contract(off)
+    const double s_uvw0 = p.f0 / kC0, s_duvw = p.df / kC0;
+    const double uvw[3] = {(double)uvws[3 * (int64_t)row],
+            (double)uvws[3 * (int64_t)row + 1],
+            (double)uvws[3 * (int64_t)row + 2]};
+    double uvw0[3] = {uvw[0] * s_uvw0, uvw[1] * s_uvw0, uvw[2] * s_uvw0};
+    const double duvw[3] = {uvw[0] * s_duvw, uvw[1] * s_duvw,
+            uvw[2] * s_duvw};
+    uvw0[0] -= off_u / p.theta;
+    uvw0[1] -= off_v / p.theta;
+    uvw0[2] -= ((p.off_w + p.w_plane - 1) * p.w_step);
+    const double uu = uvw0[0] + c * duvw[0];
+    const double vv = uvw0[1] + c * duvw[1];
+    const double ww = uvw0[2] + c * duvw[2];
+    const double theta_ov = p.theta * p.os;
+    const double w_step_ov = 1.0 / p.w_step * p.wos;
+    const int half_ov = (p.S / 2 - p.support / 2 + 1) * p.os;
+    const int iu0_ov = int(round(uu * theta_ov)) + half_ov;
+    const int iv0_ov = int(round(vv * theta_ov)) + half_ov;
+    const int iw0_ov = int(round(ww * w_step_ov));
+    Taps2 t;
+    t.iu0 = iu0_ov / p.os;
+    t.iv0 = iv0_ov / p.os;
+    t.u_off = (iu0_ov % p.os) * p.support;
+    t.v_off = (iv0_ov % p.os) * p.support;
+    t.w_off = (iw0_ov % p.wos) * p.w_support;
+    t.valid = iu0_ov >= 0 && iv0_ov >= 0 && iw0_ov >= 0;
+    return t;
+}
+
+// Offset of stack cell (layer iw of the tower, row iu, column iv) from the
+// slot's base, following the reference's flat [w_support, S, S] indexing
+// through the ring (see stack_cell in sdp_gridder_wtower_uvw.hip); -1
+// outside. The stack is layer-major: [w_support][slots][S][S], so that one
+// layer of all sub-grids is a contiguous FFT batch. *sign = checkerboard
+// sign of the cell.
+__device__ __forceinline__ int64_t tower_cell(const TowerParams& p, int iw,
+        int iu, int iv, int* sign)
+{
+    if (iu >= 0 && iu < p.S && iv >= 0 && iv < p.S)
+    {
+        *sign = parity_sign(iu + iv);
+        return ((p.ring + iw) % p.w_support) * p.layer_stride +
+                (int64_t)iu * p.S + iv;
+    }
+    const int64_t f = ((int64_t)iw * p.S + iu) * p.S + iv;
+    if (f < 0 || f >= p.w_support * p.layer) return -1;
+    const int l = (int)(f / p.layer);
+    const int64_t rem = f - l * p.layer;
+    *sign = parity_sign(rem / p.S + rem % p.S);
+    return ((p.ring + l) % p.w_support) * p.layer_stride + rem;
+}
+
+template<typename T>
+__device__ __forceinline__ T wave_sum(T x)
+{
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
+// Degrid: one wavefront per item; vis[row, c] += sum over the taps of the
+// checkerboard-corrected stack (sdp_gridder_wtower_uvw.cpp:143-171).
+template<typename T, typename U>
+__global__ __launch_bounds__(64 * kWaves)
+void k_tower_degrid(TowerParams p, const int4* __restrict__ items,
+        int64_t n_items, const U* __restrict__ uvws,
+        const Cx<T>* __restrict__ stack, const double* __restrict__ uv_kernel,
+        const double* __restrict__ w_kernel, Cx<T>* __restrict__ vis)
+{
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    const int64_t it = blockIdx.x * (int64_t)kWaves + (threadIdx.x >> 6);
+    if (it >= n_items) return;
+    const int4 item = items[it];
+    const int task = p.task[item.w];
+    const int off_u = (int)((p.min_iu + task / p.nv) * p.eff);
+    const int off_v = (int)((p.min_iv + task % p.nv) * p.eff);
+    const Cx<T>* base = stack + item.w * p.layer;
+    const int taps = p.support * p.support;
+    for (int c = item.y; c < item.z; ++c)
+    {
+        const Taps2 t = item_taps(p, uvws, item.x, c, off_u, off_v);
+        if (!t.valid) continue;
+        Cx<T> acc = cx<T>(0, 0);
+        for (int k = lane; k < taps; k += 64)
+        {
+            const int iu = k / p.support, iv = k % p.support;
+            const T ku = (T)uv_kernel[t.u_off + iu];
+            const T kv = (T)uv_kernel[t.v_off + iv];
+            for (int iw = 0; iw < p.w_support; ++iw)
+            {
+                int sgn = 1;
+                const int64_t cell = tower_cell(p, iw, t.iu0 + iu,
+                        t.iv0 + iv, &sgn);
+                if (cell < 0) continue;
+                const Cx<T> gv = base[cell];
+                const T kw = (T)w_kernel[t.w_off + iw];
+                const T gr = sgn < 0 ? -gv.re : gv.re;
+                const T gi = sgn < 0 ? -gv.im : gv.im;
+                acc.re += kw * (ku * (kv * gr));
+                acc.im += kw * (ku * (kv * gi));
+            }
+        }
+        acc.re = wave_sum(acc.re);
+        acc.im = wave_sum(acc.im);
+        if (lane == 0)
+        {
+            Cx<T>& out = vis[(int64_t)item.x * p.num_chan + c];
+            out.re += acc.re;
+            out.im += acc.im;
+        }
+    }
+}
+
+// Grid: one wavefront per item; the taps are added with device atomics to
+// the stack, pre-multiplied by the checkerboard of the inverse FFT that
+// follows (sdp_gridder_wtower_uvw.cpp:455-480).
+template<typename T, typename U>
+__global__ __launch_bounds__(64 * kWaves)
+void k_tower_grid(TowerParams p, const int4* __restrict__ items,
+        int64_t n_items, const U* __restrict__ uvws, Cx<T>* __restrict__ stack,
+        const double* __restrict__ uv_kernel,
+        const double* __restrict__ w_kernel, const Cx<T>* __restrict__ vis)
+{
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    const int64_t it = blockIdx.x * (int64_t)kWaves + (threadIdx.x >> 6);
+    if (it >= n_items) return;
+    const int4 item = items[it];
+    const int task = p.task[item.w];
+    const int off_u = (int)((p.min_iu + task / p.nv) * p.eff);
+    const int off_v = (int)((p.min_iv + task % p.nv) * p.eff);
+    Cx<T>* base = stack + item.w * p.layer;
+    const int taps = p.support * p.support;
+    for (int c = item.y; c < item.z; ++c)
+    {
+        const Taps2 t = item_taps(p, uvws, item.x, c, off_u, off_v);
+        if (!t.valid) continue;
+        const Cx<T> v = vis[(int64_t)item.x * p.num_chan + c];
+        for (int k = lane; k < taps; k += 64)
+        {
+            const int iu = k / p.support, iv = k % p.support;
+            const T ku = (T)uv_kernel[t.u_off + iu];
+            const T kv = (T)uv_kernel[t.v_off + iv];
+            for (int iw = 0; iw < p.w_support; ++iw)
+            {
+                int sgn = 1;
+                const int64_t cell = tower_cell(p, iw, t.iu0 + iu,
+                        t.iv0 + iv, &sgn);
+                if (cell < 0) continue;
+                const T kw = (T)w_kernel[t.w_off + iw];
+                const T wr = kw * v.re, wi = kw * v.im;
+                const T ur = ku * wr, ui = ku * wi;
+                T ar = kv * ur, ai = kv * ui;
+                if (sgn < 0)
+                {
+                    ar = -ar;
+                    ai = -ai;
+                }
+                unsafeAtomicAdd(&base[cell].re, ar);
+                unsafeAtomicAdd(&base[cell].im, ai);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Element-wise tower passes over `slots` sub-grids of S x S.
+
+__device__ __forceinline__ Cx<double> pattern_pow(const Cx<double>* wp,
+        int64_t i, int e)
+{
+    return (e == 1) ? wp[i] : cpow_int(wp[i], e);
+}
+
+// Gridding, one layer: wimg = wimg / D + checkerboard(IFFT(layer));
+// layer = 0 (.cpp:1029-1058).
+template<typename T>
+__global__ void k_grid_step(Cx<double>* __restrict__ wimg,
+        Cx<T>* __restrict__ layer_base, const Cx<double>* __restrict__ wp,
+        int64_t layer, int S, int64_t n, int clear)
+{
+#pragma clang fp contract(off)
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t e = i % layer;
+    Cx<T>* l = layer_base + i;
+    Cx<double> z = cdiv(wimg[i], wp[e]);
+    const int sgn = parity_sign(e / S + e % S);
+    const Cx<T> f = *l;
+    z.re += (double)(sgn < 0 ? -f.re : f.re);
+    z.im += (double)(sgn < 0 ? -f.im : f.im);
+    wimg[i] = z;
+    if (clear) *l = cx<T>(0, 0);
+}
+
+// Gridding, end of tower: sub-grid = (T)(wimg * D^e) with the checkerboard
+// of the forward FFT that follows, written to layer 0 of the slot
+// (.cpp:1102-1113 and sdp_fft_exec_shift).
+template<typename T>
+__global__ void k_grid_final(const Cx<double>* __restrict__ wimg,
+        Cx<T>* __restrict__ out, const Cx<double>* __restrict__ wp,
+        int64_t layer, int S, int e_final, int64_t n)
+{
+#pragma clang fp contract(off)
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t e = i % layer;
+    Cx<double> z = wimg[i];
+    if (e_final != 0) z = cmul(z, pattern_pow(wp, e, e_final));
+    T re = (T)z.re, im = (T)z.im;
+    if (parity_sign(e / S + e % S) < 0)
+    {
+        re = -re;
+        im = -im;
+    }
+    out[i] = cx<T>(re, im);
+}
+
+// Degridding, start of tower: wimg = (c128)(checkerboard(IFFT(cut-out)) *
+// norm) / D^e0 (.cpp:423-427 and :803-808).
+template<typename T>
+__global__ void k_degrid_init(Cx<T>* __restrict__ wimg,
+        const Cx<double>* __restrict__ wp, int64_t layer, int S, T norm,
+        int e0, int64_t n)
+{
+#pragma clang fp contract(off)
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t e = i % layer;
+    Cx<T> x = wimg[i];
+    if (parity_sign(e / S + e % S) < 0)
+    {
+        x.re = -x.re;
+        x.im = -x.im;
+    }
+    x.re *= norm;
+    x.im *= norm;
+    const Cx<double> z = cdiv(cx<double>((double)x.re, (double)x.im),
+            pattern_pow(wp, e, e0));
+    wimg[i] = cx<T>((T)z.re, (T)z.im);
+}
+
+// Degridding, one layer: layer = checkerboard(wimg) (the forward FFT
+// follows); wimg = wimg / D (.cpp:831-857).
+template<typename T>
+__global__ void k_degrid_step(Cx<T>* __restrict__ wimg,
+        Cx<T>* __restrict__ layer_base, const Cx<double>* __restrict__ wp,
+        int64_t layer, int S, int64_t n)
+{
+#pragma clang fp contract(off)
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t e = i % layer;
+    const Cx<T> x = wimg[i];
+    const bool neg = parity_sign(e / S + e % S) < 0;
+    layer_base[i] = cx<T>(neg ? -x.re : x.re, neg ? -x.im : x.im);
+    const Cx<double> z = cdiv(cx<double>((double)x.re, (double)x.im), wp[e]);
+    wimg[i] = cx<T>((T)z.re, (T)z.im);
+}
+
+// Degridding: cut the sub-grids out of the FFT'd grid
+// (sdp_gridder_subgrid_cut_out, utils.cpp:603-649) with the grid FFT's
+// output checkerboard and the sub-grid IFFT's input checkerboard; slots
+// [slots, slots_alloc) are zeroed.
+template<typename T>
+__global__ void k_cut_out(const Cx<T>* __restrict__ grid, int64_t G,
+        Cx<T>* __restrict__ wimg, int S, int64_t layer, const int* task,
+        int64_t nv, int64_t min_iu, int64_t min_iv, int eff, int64_t slots,
+        int64_t n)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t slot = i / layer, e = i - slot * layer;
+    if (slot >= slots)
+    {
+        wimg[i] = cx<T>(0, 0);
+        return;
+    }
+    const int t = task[slot];
+    const int64_t iu = min_iu + t / nv, iv = min_iv + t % nv;
+    const int64_t a = e / S, b = e % S;
+    int64_t gu = (a + G / 2 - S / 2 + iu * eff) % G;
+    int64_t gv = (b + G / 2 - S / 2 + iv * eff) % G;
+    if (gu < 0) gu += G;
+    if (gv < 0) gv += G;
+    const Cx<T> x = grid[gu * G + gv];
+    const bool neg = parity_sign(gu + gv + a + b) < 0;
+    wimg[i] = cx<T>(neg ? -x.re : x.re, neg ? -x.im : x.im);
+}
+
+__device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b)
+{
+    return a >= 0 ? a / b : -((-a + b - 1) / b);
+}
+
+// Gridding: grid (+)= sum of the FFT'd sub-grids covering each cell, in
+// the reference's task order (sdp_gridder_subgrid_add, utils.cpp:553-601,
+// sequential over tasks), with the sub-grid FFT's output checkerboard, the
+// grid IFFT's input checkerboard, and factor (image_size / S)^2.
+template<typename T>
+__global__ void k_gather_grid(Cx<T>* __restrict__ grid, int64_t G,
+        const Cx<T>* __restrict__ stack, int S,
+        const int* __restrict__ slot_of, int64_t nu, int64_t nv,
+        int64_t min_iu, int64_t min_iv, int eff, T factor, int accumulate)
+{
+#pragma clang fp contract(off)
+    const int64_t gv = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t gu = blockIdx.y;
+    if (gv >= G) return;
+    Cx<T> acc = accumulate ? grid[gu * G + gv] : cx<T>(0, 0);
+    const bool neg_g = parity_sign(gu + gv) < 0;
+    const int64_t xu = gu - G / 2 + S / 2, xv = gv - G / 2 + S / 2;
+    for (int ku = -1; ku <= 1; ++ku)
+    {
+        // Sub-grids iu with 0 <= x - iu eff < S.
+        const int64_t x = xu + ku * G;
+        const int64_t iu_lo = max(floor_div(x - S + eff, eff), min_iu);
+        const int64_t iu_hi = min(floor_div(x, eff), min_iu + nu - 1);
+        for (int64_t iu = iu_lo; iu <= iu_hi; ++iu)
+        {
+            const int64_t a = x - iu * eff;
+            if (a < 0 || a >= S) continue;
+            for (int kv = -1; kv <= 1; ++kv)
+            {
+                const int64_t y = xv + kv * G;
+                const int64_t iv_lo = max(floor_div(y - S + eff, eff),
+                        min_iv);
+                const int64_t iv_hi = min(floor_div(y, eff), min_iv + nv - 1);
+                for (int64_t iv = iv_lo; iv <= iv_hi; ++iv)
+                {
+                    const int64_t b = y - iv * eff;
+                    if (b < 0 || b >= S) continue;
+                    const int s = slot_of[(iu - min_iu) * nv + (iv - min_iv)];
+                    if (s < 0) continue;
+                    const Cx<T> x0 = stack[(int64_t)s * S * S + a * S + b];
+                    const bool neg = parity_sign(a + b) < 0;
+                    T re = (neg ? -x0.re : x0.re) * factor;
+                    T im = (neg ? -x0.im : x0.im) * factor;
+                    if (neg_g)
+                    {
+                        re = -re;
+                        im = -im;
+                    }
+                    acc.re += re;
+                    acc.im += im;
+                }
+            }
+        }
+    }
+    grid[gu * G + gv] = acc;
+}
+
+// Gridding, image side of a w-stack plane: image += grid_correct(
+// checkerboard(IFFT(grid)) / G^2) (.cpp:702-711).
+template<typename T>
+__global__ void k_image_update(const Cx<T>* __restrict__ grid, int64_t G,
+        AnyView image, T norm, CorrParams cp)
+{
+#pragma clang fp contract(off)
+    const int64_t gv = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t gu = blockIdx.y;
+    if (gv >= G) return;
+    const int64_t i = gu * G + gv;
+    Cx<T> x = grid[i];
+    if (parity_sign(gu + gv) < 0)
+    {
+        x.re = -x.re;
+        x.im = -x.im;
+    }
+    x.re *= norm;
+    x.im *= norm;
+    const Cx<double> z = correct_value(cx<double>(x.re, x.im),
+            sizeof(T) == 8 ? 3 : 2, (int)(gu - G / 2), (int)(gv - G / 2), cp);
+    Cx<double> o = image.load(i);
+    o.re += z.re;
+    if (image.kind >= 2) o.im += z.im;
+    image.store(i, o);
+}
+
+// Degridding, image side of a w-stack plane: grid = checkerboard(
+// degrid_correct((T)image)) ahead of the forward FFT (.cpp:363-375).
+template<typename T>
+__global__ void k_image_to_grid(AnyView image, int64_t G,
+        Cx<T>* __restrict__ grid, CorrParams cp)
+{
+#pragma clang fp contract(off)
+    const int64_t gv = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t gu = blockIdx.y;
+    if (gv >= G) return;
+    const int64_t i = gu * G + gv;
+    const Cx<double> a = image.load(i);
+    const Cx<double> z = correct_value(cx<double>((double)(T)a.re,
+            (double)(T)a.im), sizeof(T) == 8 ? 3 : 2, (int)(gu - G / 2),
+            (int)(gv - G / 2), cp);
+    T re = (T)z.re, im = (T)z.im;
+    if (parity_sign(gu + gv) < 0)
+    {
+        re = -re;
+        im = -im;
+    }
+    grid[i] = cx<T>(re, im);
+}
+
+// ---------------------------------------------------------------------------
+// Host side.
+
+unsigned blocks_of(int64_t n, int t = 256)
+{
+    return (unsigned)((n + t - 1) / t);
+}
+
+// Device buffers reused across calls (grown on demand).
+struct Workspace
+{
+    std::vector<std::pair<void*, size_t> > buf;
+
+    void* get(size_t id, size_t bytes, sdp_Error* status)
+    {
+        if (buf.size() <= id) buf.resize(id + 1, {nullptr, 0});
+        if (buf[id].second < bytes)
+        {
+            if (buf[id].first) (void)hipFree(buf[id].first);
+            buf[id] = {nullptr, 0};
+            SDP_HIP_CHECK(hipMalloc(&buf[id].first, bytes), status);
+            if (*status) return nullptr;
+            buf[id].second = bytes;
+        }
+        return buf[id].first;
+    }
+};
+
+enum BufId
+{
+    kRowCount, kRowOffset, kOccupied, kSlotMap, kKeys, kKeysAlt, kIdx,
+    kIdxAlt, kItemsRaw, kItems, kHist, kTemp, kTasks, kSlotOf, kBounds,
+    kStack, kWimg, kGrid, kNumBuf
+};
+
+std::mutex g_mutex;                  // one driver call at a time
+
+Workspace& workspace()
+{
+    static Workspace ws;
+    return ws;
+}
+
+sdp_fft::Plan2D* cached_plan(int n, bool dbl, size_t batch, size_t dist,
+        sdp_Error* status)
+{
+    static std::map<std::tuple<int, bool, size_t, size_t>,
+            sdp_fft::Plan2D*> cache;
+    const auto key = std::make_tuple(n, dbl, batch, dist);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    sdp_fft::Plan2D* p = sdp_fft::create_2d_batched(n, n, dbl, batch, dist,
+            status);
+    if (p) cache[key] = p;
+    return p;
+}
+
+sdp_GridderWtowerUVW* cached_kernel(int image_size, int S, double theta,
+        double w_step, double hu, double hv, int support, int os,
+        int w_support, int wos, sdp_Error* status)
+{
+    static std::map<std::tuple<int, int, double, double, double, double, int,
+            int, int, int>, sdp_GridderWtowerUVW*> cache;
+    const auto key = std::make_tuple(image_size, S, theta, w_step, hu, hv,
+            support, os, w_support, wos);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    sdp_GridderWtowerUVW* k = sdp_gridder_wtower_uvw_create(image_size, S,
+            theta, w_step, hu, hv, support, os, w_support, wos, status);
+    if (!k) return nullptr;
+    plan_ensure_correction(k, status);
+    if (*status)
+    {
+        sdp_gridder_wtower_uvw_free(k);
+        return nullptr;
+    }
+    cache[key] = k;
+    return k;
+}
+
+// One (w-stack plane, batch of sub-grids) unit of work.
+struct Group
+{
+    int64_t iw;
+    int64_t slots, slots_alloc;
+    int64_t task_base;               // into the concatenated task list
+    int64_t first_p, last_p;         // global w-layer range with items
+    bool first_of_plane, last_of_plane;
+};
+
+struct Binned
+{
+    Geo g;
+    std::vector<Group> groups;
+    std::vector<int> tasks;          // concatenated slot -> task ids
+    std::vector<int64_t> offsets;    // [groups][NP + 1] item offsets
+    int4* items = nullptr;           // sorted
+    int* d_tasks = nullptr;
+    int64_t n_items = 0;
+    int64_t t_cap = 0;
+};
+
+double now_s()
+{
+    return std::chrono::duration<double>(
+            std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Bounds of all visibilities (sdp_gridder_uvw_bounds_all with all channels,
+// .cpp:318-330), then the binning passes.
+template<typename U>
+bool bin_visibilities(const U* d_uvw, Geo& g, size_t budget_bytes,
+        size_t per_slot_bytes, Binned* out, sdp_Error* status)
+{
+    Workspace& ws = workspace();
+    const int64_t R = g.num_rows;
+    int* d_s = (int*)ws.get(kBounds, 2 * R * sizeof(int), status);
+    if (*status) return false;
+    int* d_e = d_s + R;
+    k_fill_int<<<blocks_of(2 * R), 256>>>(d_s, R, 0, (int)g.num_chan);
+    SDP_HIP_CHECK_LAUNCH(status);
+    double lo[3], hi[3];
+    uvw_bounds_dev<U>(d_uvw, R, g.f0, g.df, d_s, d_e, lo, hi, status);
+    if (*status) return false;
+    if (!(lo[0] <= hi[0])) return false;          // no visibilities
+    const double eta = 1e-5;
+    g.min_iu = (int64_t)floor(lo[0] / g.eff_dist + 0.5 - eta);
+    g.max_iu = (int64_t)floor(hi[0] / g.eff_dist + 0.5 + eta);
+    g.min_iv = (int64_t)floor(lo[1] / g.eff_dist + 0.5 - eta);
+    g.max_iv = (int64_t)floor(hi[1] / g.eff_dist + 0.5 + eta);
+    g.min_iw = (int64_t)floor(lo[2] / g.ws_dist + 0.5 - eta);
+    g.max_iw = (int64_t)floor(hi[2] / g.ws_dist + 0.5 + eta);
+    g.nu = g.max_iu - g.min_iu + 1;
+    g.nv = g.max_iv - g.min_iv + 1;
+    g.niw = g.max_iw - g.min_iw + 1;
+    g.ntask = g.nu * g.nv;
+    g.P0 = (int64_t)floor(fmin(lo[2], hi[2]) / g.w_step) - 2;
+    g.NP = (int64_t)floor(hi[2] / g.w_step) + 4 - g.P0;
+    if (g.nu * g.nv * g.niw > (int64_t)1 << 31)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Too many sub-grids (%lld x %lld x %lld w-planes)",
+                (long long)g.nu, (long long)g.nv, (long long)g.niw);
+        return false;
+    }
+
+    // Count pass.
+    int64_t* d_count = (int64_t*)ws.get(kRowCount, (R + 1) * sizeof(int64_t),
+            status);
+    unsigned char* d_occ = (unsigned char*)ws.get(kOccupied,
+            g.niw * g.ntask, status);
+    if (*status) return false;
+    SDP_HIP_CHECK(hipMemsetAsync(d_occ, 0, g.niw * g.ntask, 0), status);
+    BinOut bo = {};
+    bo.row_count = d_count;
+    bo.occupied = d_occ;
+    k_bin<U, false><<<blocks_of(R), 256>>>(d_uvw, g, bo);
+    SDP_HIP_CHECK_LAUNCH(status);
+    // Row offsets (exclusive scan of the counts).
+    int64_t* d_off = (int64_t*)ws.get(kRowOffset, (R + 1) * sizeof(int64_t),
+            status);
+    size_t temp_bytes = 0;
+    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, temp_bytes,
+            d_count, d_off, (int)(R + 1)), status);
+    void* d_temp = ws.get(kTemp, temp_bytes, status);
+    if (*status) return false;
+    SDP_HIP_CHECK(hipMemsetAsync(d_count + R, 0, sizeof(int64_t), 0),
+            status);
+    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(d_temp, temp_bytes,
+            d_count, d_off, (int)(R + 1)), status);
+    int64_t n_items = 0;
+    SDP_HIP_CHECK(hipMemcpy(&n_items, d_off + R, sizeof(int64_t),
+            hipMemcpyDeviceToHost), status);
+    std::vector<unsigned char> occ(g.niw * g.ntask);
+    SDP_HIP_CHECK(hipMemcpy(occ.data(), d_occ, occ.size(),
+            hipMemcpyDeviceToHost), status);
+    if (*status) return false;
+    if (n_items > 0x7FFFFFFF)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Too many visibility runs (%lld)", (long long)n_items);
+        return false;
+    }
+
+    // Groups: the sub-grids of each w-stack plane, in task order, in
+    // batches within the memory budget.
+    const int64_t max_slots = std::max<int64_t>(1,
+            (int64_t)(budget_bytes / per_slot_bytes));
+    std::vector<Slot> slot_map(g.niw * g.ntask, Slot{-1, -1});
+    out->groups.clear();
+    out->tasks.clear();
+    for (int64_t iw_rel = 0; iw_rel < g.niw; ++iw_rel)
+    {
+        std::vector<int> list;
+        for (int64_t t = 0; t < g.ntask; ++t)
+            if (occ[iw_rel * g.ntask + t]) list.push_back((int)t);
+        for (size_t b = 0; b < list.size(); b += max_slots)
+        {
+            Group gr;
+            gr.iw = g.min_iw + iw_rel;
+            gr.slots = std::min<int64_t>(max_slots, list.size() - b);
+            gr.slots_alloc = (gr.slots + 63) / 64 * 64;
+            gr.task_base = (int64_t)out->tasks.size();
+            gr.first_of_plane = (b == 0);
+            gr.last_of_plane = (b + gr.slots == list.size());
+            gr.first_p = gr.last_p = 0;
+            for (int64_t s = 0; s < gr.slots; ++s)
+            {
+                const int t = list[b + s];
+                out->tasks.push_back(t);
+                slot_map[iw_rel * g.ntask + t] =
+                        Slot{(int)out->groups.size(), (int)s};
+            }
+            out->groups.push_back(gr);
+        }
+    }
+    const int64_t ng = (int64_t)out->groups.size();
+    out->t_cap = 64;
+    for (const Group& gr : out->groups)
+        out->t_cap = std::max(out->t_cap, gr.slots_alloc);
+    out->n_items = n_items;
+    out->g = g;
+    if (ng == 0 || n_items == 0) return true;
+
+    // Emit pass.
+    Slot* d_map = (Slot*)ws.get(kSlotMap, slot_map.size() * sizeof(Slot),
+            status);
+    uint64_t* d_keys = (uint64_t*)ws.get(kKeys, n_items * 8, status);
+    uint64_t* d_keys2 = (uint64_t*)ws.get(kKeysAlt, n_items * 8, status);
+    uint32_t* d_idx = (uint32_t*)ws.get(kIdx, n_items * 4, status);
+    uint32_t* d_idx2 = (uint32_t*)ws.get(kIdxAlt, n_items * 4, status);
+    int4* d_raw = (int4*)ws.get(kItemsRaw, n_items * sizeof(int4), status);
+    int4* d_items = (int4*)ws.get(kItems, n_items * sizeof(int4), status);
+    unsigned int* d_hist = (unsigned int*)ws.get(kHist,
+            ng * g.NP * sizeof(unsigned int), status);
+    int* d_tasks = (int*)ws.get(kTasks, out->tasks.size() * sizeof(int),
+            status);
+    if (*status) return false;
+    SDP_HIP_CHECK(hipMemcpy(d_map, slot_map.data(),
+            slot_map.size() * sizeof(Slot), hipMemcpyHostToDevice), status);
+    SDP_HIP_CHECK(hipMemcpy(d_tasks, out->tasks.data(),
+            out->tasks.size() * sizeof(int), hipMemcpyHostToDevice), status);
+    SDP_HIP_CHECK(hipMemsetAsync(d_hist, 0, ng * g.NP * sizeof(unsigned int),
+            0), status);
+    bo = {};
+    bo.row_offset = d_off;
+    bo.slot_map = d_map;
+    bo.keys = d_keys;
+    bo.idx = d_idx;
+    bo.items = d_raw;
+    bo.hist = d_hist;
+    bo.t_cap = out->t_cap;
+    k_bin<U, true><<<blocks_of(R), 256>>>(d_uvw, g, bo);
+    SDP_HIP_CHECK_LAUNCH(status);
+    // Sort by (group, w-layer, slot).
+    const uint64_t max_key = ((uint64_t)ng * g.NP) * out->t_cap;
+    int end_bit = 1;
+    while (end_bit < 64 && (max_key >> end_bit)) ++end_bit;
+    hipcub::DoubleBuffer<uint64_t> kb(d_keys, d_keys2);
+    hipcub::DoubleBuffer<uint32_t> vb(d_idx, d_idx2);
+    temp_bytes = 0;
+    SDP_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes,
+            kb, vb, (int)n_items, 0, end_bit), status);
+    d_temp = ws.get(kTemp, temp_bytes, status);
+    if (*status) return false;
+    SDP_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(d_temp, temp_bytes,
+            kb, vb, (int)n_items, 0, end_bit), status);
+    k_gather_items<<<blocks_of(n_items), 256>>>(vb.Current(), d_raw, d_items,
+            n_items);
+    SDP_HIP_CHECK_LAUNCH(status);
+    // Item offsets per (group, w-layer).
+    std::vector<unsigned int> hist(ng * g.NP);
+    SDP_HIP_CHECK(hipMemcpy(hist.data(), d_hist, hist.size() * 4,
+            hipMemcpyDeviceToHost), status);
+    if (*status) return false;
+    out->offsets.assign(ng * (g.NP + 1), 0);
+    int64_t run = 0;
+    for (int64_t gi = 0; gi < ng; ++gi)
+    {
+        Group& gr = out->groups[gi];
+        gr.first_p = -1;
+        for (int64_t p = 0; p < g.NP; ++p)
+        {
+            out->offsets[gi * (g.NP + 1) + p] = run;
+            const unsigned int c = hist[gi * g.NP + p];
+            if (c)
+            {
+                if (gr.first_p < 0) gr.first_p = p;
+                gr.last_p = p;
+            }
+            run += c;
+        }
+        out->offsets[gi * (g.NP + 1) + g.NP] = run;
+    }
+    out->items = d_items;
+    out->d_tasks = d_tasks;
+    return true;
+}
+
+TowerParams tower_params(const sdp_GridderWtowerUVW* k, const Geo& g,
+        const Group& gr, const Binned& b)
+{
+    TowerParams p;
+    p.S = g.S;
+    p.support = k->support;
+    p.w_support = k->w_support;
+    p.os = k->oversampling;
+    p.wos = k->w_oversampling;
+    p.theta = g.theta;
+    p.w_step = g.w_step;
+    p.f0 = g.f0;
+    p.df = g.df;
+    p.num_chan = g.num_chan;
+    p.off_w = (int)(gr.iw * g.H);
+    p.w_plane = 0;
+    p.ring = 0;
+    p.layer = (int64_t)g.S * g.S;
+    p.layer_stride = p.layer * gr.slots_alloc;
+    p.task = b.d_tasks + gr.task_base;
+    p.nv = g.nv;
+    p.min_iu = g.min_iu;
+    p.min_iv = g.min_iv;
+    p.eff = g.eff;
+    return p;
+}
+
+struct Timing
+{
+    double bin = 0, towers = 0, image = 0;
+    int64_t layers = 0;
+};
+
+// Grid all visibilities of the selected w-stack planes.
+template<typename T, typename U>
+void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
+        const U* d_uvw, AnyView image, int64_t G, int verbosity,
+        sdp_Error* status)
+{
+    Workspace& ws = workspace();
+    Timing tm;
+    double t0 = now_s();
+    const int64_t layer = (int64_t)g.S * g.S;
+    const size_t per_slot = layer * (size_t)(g.w_support * sizeof(Cx<T>) +
+            sizeof(Cx<double>));
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    const size_t budget = std::max<size_t>(per_slot * 64, free_b / 3);
+    Binned b;
+    const bool any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b,
+            status);
+    if (*status) return;
+    if (verbosity > 0)
+    {
+        (void)hipDeviceSynchronize();
+        tm.bin = now_s() - t0;
+    }
+    g = b.g;
+    if (!any || b.groups.empty()) return;
+    Cx<T>* d_stack = (Cx<T>*)ws.get(kStack,
+            b.t_cap * layer * g.w_support * sizeof(Cx<T>), status);
+    Cx<double>* d_wimg = (Cx<double>*)ws.get(kWimg,
+            b.t_cap * layer * sizeof(Cx<double>), status);
+    Cx<T>* d_grid = (Cx<T>*)ws.get(kGrid, G * G * sizeof(Cx<T>), status);
+    int* d_slot_of = (int*)ws.get(kSlotOf, g.ntask * sizeof(int), status);
+    sdp_fft::Plan2D* big = cached_plan((int)G, sizeof(T) == 8, 1, G * G,
+            status);
+    if (*status) return;
+    const Cx<double>* wp = (const Cx<double>*)k->d_w_pattern;
+    const int ws_n = g.w_support;
+    const T factor = (T)((double)k->image_size / g.S *
+            ((double)k->image_size / g.S));
+    std::vector<int> slot_of(g.ntask);
+    for (size_t gi = 0; gi < b.groups.size() && !*status; ++gi)
+    {
+        const Group& gr = b.groups[gi];
+        const double tg = now_s();
+        if (verbosity > 1)
+            SDP_LOG_INFO("group %zu: w-stack plane %lld, %lld sub-grids, "
+                    "w-layers %lld..%lld (relative), items %lld..%lld", gi,
+                    (long long)gr.iw, (long long)gr.slots,
+                    (long long)(gr.first_p + g.P0 - (int)(gr.iw * g.H)),
+                    (long long)(gr.last_p + g.P0 - (int)(gr.iw * g.H)),
+                    (long long)b.offsets[gi * (g.NP + 1)],
+                    (long long)b.offsets[gi * (g.NP + 1) + g.NP]);
+        sdp_fft::Plan2D* sp = cached_plan(g.S, sizeof(T) == 8,
+                gr.slots_alloc, layer, status);
+        if (*status) break;
+        TowerParams p = tower_params(k, g, gr, b);
+        const int64_t n_el = gr.slots * layer;
+        const int64_t ls = p.layer_stride;
+        const bool empty = gr.first_p < 0;   // no visibility survived
+        SDP_HIP_CHECK(hipMemsetAsync(d_stack, 0,
+                gr.slots_alloc * layer * ws_n * sizeof(Cx<T>), 0), status);
+        SDP_HIP_CHECK(hipMemsetAsync(d_wimg, 0, n_el * sizeof(Cx<double>),
+                0), status);
+        const int64_t first = empty ? 0 : gr.first_p + g.P0 - p.off_w;
+        const int64_t last = empty ? -1 : gr.last_p + g.P0 - p.off_w;
+        int ring = 0;
+        for (int64_t w_plane = first; w_plane <= last && !*status; ++w_plane)
+        {
+            if (w_plane != first)
+            {
+                sdp_fft::exec_2d(sp, d_stack + ring * ls, false, 0, status);
+                k_grid_step<T><<<blocks_of(n_el), 256>>>(d_wimg,
+                        d_stack + ring * ls, wp, layer, g.S, n_el, 1);
+                ring = (ring + 1) % ws_n;
+            }
+            const int64_t prel = w_plane + p.off_w - g.P0;
+            const int64_t i0 = b.offsets[gi * (g.NP + 1) + prel];
+            const int64_t i1 = b.offsets[gi * (g.NP + 1) + prel + 1];
+            if (i1 > i0)
+            {
+                p.w_plane = (int)w_plane;
+                p.ring = ring;
+                k_tower_grid<T, U><<<blocks_of(i1 - i0, kWaves),
+                        64 * kWaves>>>(p, b.items + i0, i1 - i0, d_uvw,
+                        d_stack, k->d_uv_kernel, k->d_w_kernel, d_vis);
+            }
+            SDP_HIP_CHECK_LAUNCH(status);
+        }
+        for (int i = 0; i < ws_n && !*status && !empty; ++i)
+        {
+            const int l = (ring + i) % ws_n;
+            sdp_fft::exec_2d(sp, d_stack + l * ls, false, 0, status);
+            k_grid_step<T><<<blocks_of(n_el), 256>>>(d_wimg, d_stack + l * ls,
+                    wp, layer, g.S, n_el, 0);
+        }
+        tm.layers += (last - first + 1) * gr.slots;
+        if (!empty)
+        {
+            k_grid_final<T><<<blocks_of(n_el), 256>>>(d_wimg, d_stack, wp,
+                    layer, g.S, (int)(last + ws_n / 2 - 1), n_el);
+            sdp_fft::exec_2d(sp, d_stack, true, 0, status);
+        }
+        // Sub-grids into the grid.
+        std::fill(slot_of.begin(), slot_of.end(), -1);
+        for (int64_t s = 0; s < gr.slots; ++s)
+            slot_of[b.tasks[gr.task_base + s]] = (int)s;
+        SDP_HIP_CHECK(hipMemcpyAsync(d_slot_of, slot_of.data(),
+                g.ntask * sizeof(int), hipMemcpyHostToDevice, 0), status);
+        k_gather_grid<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(d_grid, G,
+                d_stack, g.S, d_slot_of, g.nu, g.nv, g.min_iu,
+                g.min_iv, g.eff, factor, gr.first_of_plane ? 0 : 1);
+        SDP_HIP_CHECK_LAUNCH(status);
+        if (verbosity > 0)
+        {
+            (void)hipDeviceSynchronize();
+            tm.towers += now_s() - tg;
+        }
+        if (gr.last_of_plane)
+        {
+            const double ti = now_s();
+            sdp_fft::exec_2d(big, d_grid, false, 0, status);
+            const CorrParams cp = corr_params(k, (int)(gr.iw * g.H), true);
+            k_image_update<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
+                    d_grid, G, image, (T)(1.0 / ((double)G * G)), cp);
+            SDP_HIP_CHECK_LAUNCH(status);
+            if (verbosity > 0)
+            {
+                (void)hipDeviceSynchronize();
+                tm.image += now_s() - ti;
+            }
+        }
+    }
+    if (verbosity > 0 && !*status)
+    {
+        SDP_LOG_INFO("w-stacking with w-towers (gridding): %lld w-stack "
+                "planes, %lld sub-grids x %lld, %zu sub-grid groups, %lld "
+                "visibility runs, %lld sub-grid w-layers",
+                (long long)g.niw, (long long)g.nu, (long long)g.nv,
+                b.groups.size(), (long long)b.n_items, (long long)tm.layers);
+        SDP_LOG_INFO("| binning %.3f s | towers %.3f s | image side %.3f s",
+                tm.bin, tm.towers, tm.image);
+    }
+}
+
+// Degrid all visibilities of the selected w-stack planes.
+template<typename T, typename U>
+void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
+        int64_t G, const U* d_uvw, Cx<T>* d_vis, int verbosity,
+        sdp_Error* status)
+{
+    Workspace& ws = workspace();
+    Timing tm;
+    double t0 = now_s();
+    const int64_t layer = (int64_t)g.S * g.S;
+    const size_t per_slot = layer * (size_t)((g.w_support + 1) *
+            sizeof(Cx<T>));
+    size_t free_b = 0, total_b = 0;
+    (void)hipMemGetInfo(&free_b, &total_b);
+    const size_t budget = std::max<size_t>(per_slot * 64, free_b / 3);
+    Binned b;
+    const bool any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b,
+            status);
+    if (*status) return;
+    if (verbosity > 0)
+    {
+        (void)hipDeviceSynchronize();
+        tm.bin = now_s() - t0;
+    }
+    g = b.g;
+    if (!any || b.groups.empty()) return;
+    Cx<T>* d_stack = (Cx<T>*)ws.get(kStack,
+            b.t_cap * layer * g.w_support * sizeof(Cx<T>), status);
+    Cx<T>* d_wimg = (Cx<T>*)ws.get(kWimg, b.t_cap * layer * sizeof(Cx<T>),
+            status);
+    Cx<T>* d_grid = (Cx<T>*)ws.get(kGrid, G * G * sizeof(Cx<T>), status);
+    sdp_fft::Plan2D* big = cached_plan((int)G, sizeof(T) == 8, 1, G * G,
+            status);
+    if (*status) return;
+    const Cx<double>* wp = (const Cx<double>*)k->d_w_pattern;
+    const int ws_n = g.w_support;
+    const T norm = (T)(1.0 / ((double)g.S * g.S));
+    for (size_t gi = 0; gi < b.groups.size() && !*status; ++gi)
+    {
+        const Group& gr = b.groups[gi];
+        if (gr.first_of_plane)
+        {
+            const double ti = now_s();
+            const CorrParams cp = corr_params(k, (int)(gr.iw * g.H), false);
+            k_image_to_grid<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
+                    image, G, d_grid, cp);
+            SDP_HIP_CHECK_LAUNCH(status);
+            sdp_fft::exec_2d(big, d_grid, true, 0, status);
+            if (verbosity > 0)
+            {
+                (void)hipDeviceSynchronize();
+                tm.image += now_s() - ti;
+            }
+        }
+        const double tg = now_s();
+        if (verbosity > 1)
+            SDP_LOG_INFO("group %zu: w-stack plane %lld, %lld sub-grids, "
+                    "w-layers %lld..%lld (relative), items %lld..%lld", gi,
+                    (long long)gr.iw, (long long)gr.slots,
+                    (long long)(gr.first_p + g.P0 - (int)(gr.iw * g.H)),
+                    (long long)(gr.last_p + g.P0 - (int)(gr.iw * g.H)),
+                    (long long)b.offsets[gi * (g.NP + 1)],
+                    (long long)b.offsets[gi * (g.NP + 1) + g.NP]);
+        if (gr.first_p < 0) continue;        // no visibility survived
+        sdp_fft::Plan2D* sp = cached_plan(g.S, sizeof(T) == 8,
+                gr.slots_alloc, layer, status);
+        if (*status) break;
+        TowerParams p = tower_params(k, g, gr, b);
+        const int64_t n_el = gr.slots * layer;
+        const int64_t n_alloc = gr.slots_alloc * layer;
+        const int64_t ls = p.layer_stride;
+        k_cut_out<T><<<blocks_of(n_alloc), 256>>>(d_grid, G, d_wimg, g.S,
+                layer, p.task, g.nv, g.min_iu, g.min_iv, g.eff, gr.slots,
+                n_alloc);
+        sdp_fft::exec_2d(sp, d_wimg, false, 0, status);
+        const int64_t first = gr.first_p + g.P0 - p.off_w;
+        const int64_t last = gr.last_p + g.P0 - p.off_w;
+        k_degrid_init<T><<<blocks_of(n_el), 256>>>(d_wimg, wp, layer, g.S,
+                norm, (int)(first - ws_n / 2), n_el);
+        for (int i = 0; i < ws_n && !*status; ++i)
+        {
+            k_degrid_step<T><<<blocks_of(n_el), 256>>>(d_wimg,
+                    d_stack + i * ls, wp, layer, g.S, n_el);
+            sdp_fft::exec_2d(sp, d_stack + i * ls, true, 0, status);
+        }
+        int ring = 0;
+        for (int64_t w_plane = first; w_plane <= last && !*status; ++w_plane)
+        {
+            if (w_plane != first)
+            {
+                const int slot_layer = ring;
+                ring = (ring + 1) % ws_n;
+                k_degrid_step<T><<<blocks_of(n_el), 256>>>(d_wimg,
+                        d_stack + slot_layer * ls, wp, layer, g.S, n_el);
+                sdp_fft::exec_2d(sp, d_stack + slot_layer * ls, true, 0,
+                        status);
+            }
+            const int64_t prel = w_plane + p.off_w - g.P0;
+            const int64_t i0 = b.offsets[gi * (g.NP + 1) + prel];
+            const int64_t i1 = b.offsets[gi * (g.NP + 1) + prel + 1];
+            if (i1 > i0)
+            {
+                p.w_plane = (int)w_plane;
+                p.ring = ring;
+                k_tower_degrid<T, U><<<blocks_of(i1 - i0, kWaves),
+                        64 * kWaves>>>(p, b.items + i0, i1 - i0, d_uvw,
+                        d_stack, k->d_uv_kernel, k->d_w_kernel, d_vis);
+            }
+            SDP_HIP_CHECK_LAUNCH(status);
+        }
+        tm.layers += (last - first + 1) * gr.slots;
+        if (verbosity > 0)
+        {
+            (void)hipDeviceSynchronize();
+            tm.towers += now_s() - tg;
+        }
+    }
+    if (verbosity > 0 && !*status)
+    {
+        SDP_LOG_INFO("w-stacking with w-towers (degridding): %lld w-stack "
+                "planes, %lld sub-grids x %lld, %zu sub-grid groups, %lld "
+                "visibility runs, %lld sub-grid w-layers",
+                (long long)g.niw, (long long)g.nu, (long long)g.nv,
+                b.groups.size(), (long long)b.n_items, (long long)tm.layers);
+        SDP_LOG_INFO("| binning %.3f s | towers %.3f s | image side %.3f s",
+                tm.bin, tm.towers, tm.image);
+    }
+}
+
+// Argument checks shared by grid_all and degrid_all (.cpp:241-259).
+bool check_args(const sdp_Mem* vis, const sdp_Mem* uvw, const sdp_Mem* image,
+        int subgrid_size, double w_tower_height, int plane_offset,
+        int plane_stride, sdp_Error* status)
+{
+    if (*status) return false;
+    const sdp_MemLocation loc = sdp_mem_location(vis);
+    if (sdp_mem_location(image) != loc || sdp_mem_location(uvw) != loc)
+    {
+        *status = SDP_ERR_MEM_LOCATION;
+        SDP_LOG_ERROR("All arrays must be in the same memory space");
+        return false;
+    }
+    if (sdp_mem_num_dims(vis) != 2 || sdp_mem_num_dims(uvw) != 2)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Visibilities and (u,v,w)-coordinates must be 2D");
+        return false;
+    }
+    if (w_tower_height == 0.0)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Automatic w-tower height not yet implemented");
+        return false;
+    }
+    if (sdp_mem_shape_dim(uvw, 1) != 3 ||
+            sdp_mem_shape_dim(uvw, 0) != sdp_mem_shape_dim(vis, 0) ||
+            sdp_mem_num_dims(image) != 2 ||
+            sdp_mem_shape_dim(image, 0) != sdp_mem_shape_dim(image, 1) ||
+            !sdp_mem_is_c_contiguous(vis) || !sdp_mem_is_c_contiguous(uvw) ||
+            !sdp_mem_is_c_contiguous(image) || subgrid_size <= 0 ||
+            subgrid_size % 2 != 0 ||
+            subgrid_size > sdp_mem_shape_dim(image, 0) || plane_stride < 1 ||
+            plane_offset < 0 || plane_offset >= plane_stride)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Inconsistent arguments: uvw must be [rows, 3], vis "
+                "[rows, chans], the image square and at least the (even) "
+                "sub-grid size, all C-contiguous");
+        return false;
+    }
+    if (sdp_mem_shape_dim(vis, 0) > 0x7FFFFFFF ||
+            sdp_mem_shape_dim(vis, 1) > 0x7FFFFFFF)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        return false;
+    }
+    const sdp_MemType tv = sdp_mem_type(vis), tu = sdp_mem_type(uvw);
+    const bool ok = (tv == SDP_MEM_COMPLEX_DOUBLE && tu == SDP_MEM_DOUBLE) ||
+            (tv == SDP_MEM_COMPLEX_FLOAT && tu == SDP_MEM_DOUBLE) ||
+            (tv == SDP_MEM_COMPLEX_FLOAT && tu == SDP_MEM_FLOAT);
+    if (!ok || any_kind(sdp_mem_type(image)) < 0)
+    {
+        *status = SDP_ERR_DATA_TYPE;
+        SDP_LOG_ERROR("Unsupported data types: vis %s, uvw %s, image %s",
+                sdp_mem_type_name(tv), sdp_mem_type_name(tu),
+                sdp_mem_type_name(sdp_mem_type(image)));
+        return false;
+    }
+    if (!sdp_hip::device_available())
+    {
+        *status = SDP_ERR_MEM_LOCATION;
+        SDP_LOG_ERROR("No GPU available for the w-towers driver.");
+        return false;
+    }
+    return true;
+}
+
+Geo make_geo(const sdp_Mem* vis, double f0, double df, int S, double theta,
+        double w_step, int support, int w_support, double subgrid_frac,
+        double H, int plane_offset, int plane_stride)
+{
+    Geo g = {};
+    g.f0 = f0;
+    g.df = df;
+    g.num_rows = sdp_mem_shape_dim(vis, 0);
+    g.num_chan = sdp_mem_shape_dim(vis, 1);
+    g.S = S;
+    if (subgrid_frac == 0.0) subgrid_frac = 2.0 / 3.0;
+    g.eff = int(floor(S * subgrid_frac));
+    g.support = support;
+    g.w_support = w_support;
+    g.theta = theta;
+    g.w_step = w_step;
+    g.H = H;
+    g.eff_dist = g.eff / theta;
+    g.ws_dist = H * w_step;
+    g.plane_offset = plane_offset;
+    g.plane_stride = plane_stride;
+    return g;
+}
+
+template<typename U>
+const U* cptr(const sdp_Mem* m)
+{
+    return (const U*)sdp_mem_data_const(m);
+}
+
+void run_grid(const sdp_Mem* vis, double f0, double df, const sdp_Mem* uvw,
+        int S, double theta, double w_step, double hu, double hv,
+        int support, int os, int w_support, int wos, double frac, double H,
+        int verbosity, sdp_Mem* image, int plane_offset, int plane_stride,
+        sdp_Error* status)
+{
+    if (!check_args(vis, uvw, image, S, H, plane_offset, plane_stride,
+            status))
+        return;
+    std::lock_guard<std::mutex> lock(g_mutex);
+    const int64_t G = sdp_mem_shape_dim(image, 0);
+    sdp_GridderWtowerUVW* k = cached_kernel((int)G, S, theta, w_step, hu, hv,
+            support, os, w_support, wos, status);
+    if (*status) return;
+    Staged sv, su, si;
+    sv.init(vis, status);
+    su.init(uvw, status);
+    si.init(image, status);
+    if (*status) return;
+    // Output image cleared first (.cpp:604-606).
+    SDP_HIP_CHECK(hipMemsetAsync(sdp_mem_data(si.dev), 0,
+            sdp_mem_num_elements(image) *
+            sdp_mem_type_size(sdp_mem_type(image)), 0), status);
+    Geo g = make_geo(vis, f0, df, S, theta, w_step, support, w_support, frac,
+            H, plane_offset, plane_stride);
+    const AnyView img = {sdp_mem_data(si.dev),
+            any_kind(sdp_mem_type(image))};
+    const sdp_MemType tv = sdp_mem_type(vis), tu = sdp_mem_type(uvw);
+    if (g.num_rows > 0 && g.num_chan > 0)
+    {
+        if (tv == SDP_MEM_COMPLEX_DOUBLE)
+            grid_all_impl<double, double>(k, g,
+                    cptr<Cx<double> >(sv.dev), cptr<double>(su.dev), img, G,
+                    verbosity, status);
+        else if (tu == SDP_MEM_DOUBLE)
+            grid_all_impl<float, double>(k, g, cptr<Cx<float> >(sv.dev),
+                    cptr<double>(su.dev), img, G, verbosity, status);
+        else
+            grid_all_impl<float, float>(k, g, cptr<Cx<float> >(sv.dev),
+                    cptr<float>(su.dev), img, G, verbosity, status);
+    }
+    si.write_back(status);
+}
+
+void run_degrid(const sdp_Mem* image, double f0, double df,
+        const sdp_Mem* uvw, int S, double theta, double w_step, double hu,
+        double hv, int support, int os, int w_support, int wos, double frac,
+        double H, int verbosity, sdp_Mem* vis, int plane_offset,
+        int plane_stride, sdp_Error* status)
+{
+    if (!check_args(vis, uvw, image, S, H, plane_offset, plane_stride,
+            status))
+        return;
+    std::lock_guard<std::mutex> lock(g_mutex);
+    const int64_t G = sdp_mem_shape_dim(image, 0);
+    sdp_GridderWtowerUVW* k = cached_kernel((int)G, S, theta, w_step, hu, hv,
+            support, os, w_support, wos, status);
+    if (*status) return;
+    Staged sv, su, si;
+    sv.init(vis, status);
+    su.init(uvw, status);
+    si.init(image, status);
+    if (*status) return;
+    // Output visibilities cleared first (.cpp:332-334).
+    SDP_HIP_CHECK(hipMemsetAsync(sdp_mem_data(sv.dev), 0,
+            sdp_mem_num_elements(vis) * sdp_mem_type_size(sdp_mem_type(vis)),
+            0), status);
+    Geo g = make_geo(vis, f0, df, S, theta, w_step, support, w_support, frac,
+            H, plane_offset, plane_stride);
+    const AnyView img = {sdp_mem_data(si.dev),
+            any_kind(sdp_mem_type(image))};
+    const sdp_MemType tv = sdp_mem_type(vis), tu = sdp_mem_type(uvw);
+    if (g.num_rows > 0 && g.num_chan > 0)
+    {
+        if (tv == SDP_MEM_COMPLEX_DOUBLE)
+            degrid_all_impl<double, double>(k, g, img, G,
+                    cptr<double>(su.dev), (Cx<double>*)sdp_mem_data(sv.dev),
+                    verbosity, status);
+        else if (tu == SDP_MEM_DOUBLE)
+            degrid_all_impl<float, double>(k, g, img, G,
+                    cptr<double>(su.dev), (Cx<float>*)sdp_mem_data(sv.dev),
+                    verbosity, status);
+        else
+            degrid_all_impl<float, float>(k, g, img, G, cptr<float>(su.dev),
+                    (Cx<float>*)sdp_mem_data(sv.dev), verbosity, status);
+    }
+    sv.write_back(status);
+}
+
+} // namespace
+
+extern "C" {
+
+void sdp_grid_wstack_wtower_grid_all(const sdp_Mem* vis, double freq0_hz,
+        double dfreq_hz, const sdp_Mem* uvw, int subgrid_size, double theta,
+        double w_step, double shear_u, double shear_v, int support,
+        int oversampling, int w_support, int w_oversampling,
+        double subgrid_frac, double w_tower_height, int verbosity,
+        sdp_Mem* image, int num_threads, sdp_Error* status)
+{
+    (void)num_threads;
+    run_grid(vis, freq0_hz, dfreq_hz, uvw, subgrid_size, theta, w_step,
+            shear_u, shear_v, support, oversampling, w_support,
+            w_oversampling, subgrid_frac, w_tower_height, verbosity, image, 0,
+            1, status);
+}
+
+void sdp_grid_wstack_wtower_degrid_all(const sdp_Mem* image,
+        double freq0_hz, double dfreq_hz, const sdp_Mem* uvw,
+        int subgrid_size, double theta, double w_step, double shear_u,
+        double shear_v, int support, int oversampling, int w_support,
+        int w_oversampling, double subgrid_frac, double w_tower_height,
+        int verbosity, sdp_Mem* vis, int num_threads, sdp_Error* status)
+{
+    (void)num_threads;
+    run_degrid(image, freq0_hz, dfreq_hz, uvw, subgrid_size, theta, w_step,
+            shear_u, shear_v, support, oversampling, w_support,
+            w_oversampling, subgrid_frac, w_tower_height, verbosity, vis, 0,
+            1, status);
+}
+
+void sdp_grid_wstack_wtower_grid_planes(const sdp_Mem* vis, double freq0_hz,
+        double dfreq_hz, const sdp_Mem* uvw, int subgrid_size, double theta,
+        double w_step, double shear_u, double shear_v, int support,
+        int oversampling, int w_support, int w_oversampling,
+        double subgrid_frac, double w_tower_height, int verbosity,
+        sdp_Mem* image, int plane_offset, int plane_stride, sdp_Error* status)
+{
+    run_grid(vis, freq0_hz, dfreq_hz, uvw, subgrid_size, theta, w_step,
+            shear_u, shear_v, support, oversampling, w_support,
+            w_oversampling, subgrid_frac, w_tower_height, verbosity, image,
+            plane_offset, plane_stride, status);
+}
+
+void sdp_grid_wstack_wtower_degrid_planes(const sdp_Mem* image,
+        double freq0_hz, double dfreq_hz, const sdp_Mem* uvw,
+        int subgrid_size, double theta, double w_step, double shear_u,
+        double shear_v, int support, int oversampling, int w_support,
+        int w_oversampling, double subgrid_frac, double w_tower_height,
+        int verbosity, sdp_Mem* vis, int plane_offset, int plane_stride,
+        sdp_Error* status)
+{
+    run_degrid(image, freq0_hz, dfreq_hz, uvw, subgrid_size, theta, w_step,
+            shear_u, shear_v, support, oversampling, w_support,
+            w_oversampling, subgrid_frac, w_tower_height, verbosity, vis,
+            plane_offset, plane_stride, status);
+}
+
+} // extern "C"

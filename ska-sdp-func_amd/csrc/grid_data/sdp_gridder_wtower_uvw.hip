@@ -21,39 +21,12 @@
 #include "wtower_dev.h"
 #include "wtower_math.h"
 #include "wtower_ops.h"
+#include "wtower_plan.h"
 #include "../fft/fft2d.h"
 #include "../utility/sdp_hip.h"
 
 using namespace sdp_wt;
 
-struct sdp_GridderWtowerUVW
-{
-    int image_size;
-    int subgrid_size;
-    double theta;
-    double w_step;
-    double shear_u;
-    double shear_v;
-    int support;
-    int oversampling;
-    int w_support;
-    int w_oversampling;
-    int num_w_planes[2];
-    std::vector<double>* uv_kernel;
-    std::vector<double>* w_kernel;
-    std::vector<double>* w_pattern;       // interleaved complex double
-    // Device copies (created on first use).
-    double* d_uv_kernel;
-    double* d_w_kernel;
-    double* d_w_pattern;
-    // Grid-correction tables (created on first use).
-    double* d_pswf_lm;                    // [image_size]
-    double* d_pswf_n;                     // Legendre coefficients
-    int n_pswf_n;
-    // Per-precision scratch: stack [w_support, S, S], w image, FFT buffer.
-    void* d_scratch[2];
-    sdp_fft::Plan2D* fft[2];
-};
 
 namespace {
 
@@ -303,74 +276,16 @@ __global__ void k_wt_grid(WtParams p, Cx<T>* __restrict__ stack,
     }
 }
 
-// Grid correction (sdp_gridder_grid_correct.cpp:18-116): 1 / (pswf(l)
-// pswf(m) pswf_n(n)), then the w-stack phasor for complex facets.
+// Grid correction of a facet (sdp_gridder_grid_correct.cpp:18-116).
 __global__ void k_grid_correct(AnyView facet, int nl, int nm, int off_l,
-        int off_m, int image_size, double theta, double w_step,
-        double shear_u, double shear_v, const double* __restrict__ pswf_lm,
-        const double* __restrict__ pswf_n, int n_pswf_n, double c_n,
-        int w_offset, int inverse, int is_complex)
+        int off_m, CorrParams cp)
 {
-#pragma clang fp contract(off)
     const int im = blockIdx.x * blockDim.x + threadIdx.x;
     const int il = blockIdx.y;
     if (im >= nm || il >= nl) return;
-    const int pl = il - nl / 2 + off_l;
-    const int pm = im - nm / 2 + off_m;
-    const double l = pl * theta / image_size;
-    const double m = pm * theta / image_size;
-    // Pixels outside the image (undefined in the reference) stay as they
-    // are.
-    if (pl + image_size / 2 < 0 || pl + image_size / 2 >= image_size ||
-            pm + image_size / 2 < 0 || pm + image_size / 2 >= image_size)
-        return;
-    const double p_l = pswf_lm[pl + image_size / 2];
-    const double p_m = pswf_lm[pm + image_size / 2];
-    double p_n = 1.0;
-    const double n = lm_to_n_dev(l, m, shear_u, shear_v);
-    if (c_n > 0.0)
-    {
-        const double n_x = fabs(n * 2.0 * w_step);
-        p_n = (n_x < 1.0) ? pswf_eval(pswf_n, n_pswf_n, n_x) : 1.0;
-    }
-    const double scale = 1.0 / (p_l * p_m * p_n);
     const int64_t i = (int64_t)il * nm + im;
-    Cx<double> z = facet.load(i);
-    if (facet.kind <= 1)
-    {
-        z.re *= (facet.kind == 0) ? (double)(float)scale : scale;
-        facet.store(i, z);
-        return;
-    }
-    if (facet.kind == 2)
-    {
-        const float s = (float)scale;
-        z.re = (double)((float)z.re * s);
-        z.im = (double)((float)z.im * s);
-    }
-    else
-    {
-        z.re *= scale;
-        z.im *= scale;
-    }
-    if (is_complex && w_offset != 0)
-    {
-        const double phase = 2.0 * M_PI * w_step * n * w_offset;
-        Cx<double> w = cx<double>(cos(phase), sin(phase));
-        if (!inverse) w = cdiv(cx<double>(1.0, 0.0), w);
-        if (facet.kind == 2)
-        {
-            const float wr = (float)w.re, wi = (float)w.im;
-            const float zr = (float)z.re, zi = (float)z.im;
-            z.re = zr * wr - zi * wi;
-            z.im = zr * wi + zi * wr;
-        }
-        else
-        {
-            z = cmul(z, w);
-        }
-    }
-    facet.store(i, z);
+    facet.store(i, correct_value(facet.load(i), facet.kind,
+            il - nl / 2 + off_l, im - nm / 2 + off_m, cp));
 }
 
 void upload(const std::vector<double>& h, double** d, sdp_Error* status)
@@ -380,20 +295,6 @@ void upload(const std::vector<double>& h, double** d, sdp_Error* status)
     if (*status) return;
     SDP_HIP_CHECK(hipMemcpy(*d, h.data(), h.size() * sizeof(double),
             hipMemcpyHostToDevice), status);
-}
-
-void ensure_device(sdp_GridderWtowerUVW* plan, sdp_Error* status)
-{
-    if (*status) return;
-    if (!sdp_hip::device_available())
-    {
-        *status = SDP_ERR_MEM_LOCATION;
-        SDP_LOG_ERROR("No GPU available for the w-towers gridder.");
-        return;
-    }
-    upload(*plan->uv_kernel, &plan->d_uv_kernel, status);
-    upload(*plan->w_kernel, &plan->d_w_kernel, status);
-    upload(*plan->w_pattern, &plan->d_w_pattern, status);
 }
 
 template<typename T>
@@ -664,15 +565,7 @@ void correct(sdp_GridderWtowerUVW* plan, sdp_Mem* facet, int off_l,
         int off_m, int w_offset, bool inverse, sdp_Error* status)
 {
     if (*status) return;
-    ensure_device(plan, status);
-    if (!plan->d_pswf_lm && !*status)
-    {
-        upload(generate_pswf(plan->support * (M_PI / 2), plan->image_size,
-                true), &plan->d_pswf_lm, status);
-        const Pswf pn = make_pswf(plan->w_support * (M_PI / 2));
-        upload(pn.coef, &plan->d_pswf_n, status);
-        plan->n_pswf_n = (int)pn.coef.size();
-    }
+    plan_ensure_correction(plan, status);
     const int kind = any_kind(sdp_mem_type(facet));
     if (kind < 0 || sdp_mem_num_dims(facet) != 2 ||
             !sdp_mem_is_c_contiguous(facet))
@@ -690,15 +583,59 @@ void correct(sdp_GridderWtowerUVW* plan, sdp_Mem* facet, int off_l,
     const AnyView v = {sdp_mem_data(f.dev), kind};
     const dim3 blocks((nm + 255) / 256, nl);
     k_grid_correct<<<blocks, 256>>>(v, nl, nm, off_l, off_m,
-            plan->image_size, plan->theta, plan->w_step, plan->shear_u,
-            plan->shear_v, plan->d_pswf_lm, plan->d_pswf_n, plan->n_pswf_n,
-            plan->w_support * (M_PI / 2), w_offset, inverse ? 1 : 0,
-            kind >= 2 ? 1 : 0);
+            corr_params(plan, w_offset, inverse));
     SDP_HIP_CHECK_LAUNCH(status);
     f.write_back(status);
 }
 
 } // namespace
+
+namespace sdp_wt {
+
+void plan_ensure_device(sdp_GridderWtowerUVW* plan, sdp_Error* status)
+{
+    if (*status) return;
+    if (!sdp_hip::device_available())
+    {
+        *status = SDP_ERR_MEM_LOCATION;
+        SDP_LOG_ERROR("No GPU available for the w-towers gridder.");
+        return;
+    }
+    upload(*plan->uv_kernel, &plan->d_uv_kernel, status);
+    upload(*plan->w_kernel, &plan->d_w_kernel, status);
+    upload(*plan->w_pattern, &plan->d_w_pattern, status);
+}
+
+void plan_ensure_correction(sdp_GridderWtowerUVW* plan, sdp_Error* status)
+{
+    plan_ensure_device(plan, status);
+    if (plan->d_pswf_lm || *status) return;
+    upload(generate_pswf(plan->support * (M_PI / 2), plan->image_size, true),
+            &plan->d_pswf_lm, status);
+    const Pswf pn = make_pswf(plan->w_support * (M_PI / 2));
+    upload(pn.coef, &plan->d_pswf_n, status);
+    plan->n_pswf_n = (int)pn.coef.size();
+}
+
+CorrParams corr_params(const sdp_GridderWtowerUVW* plan, int w_offset,
+        bool inverse)
+{
+    CorrParams cp;
+    cp.image_size = plan->image_size;
+    cp.theta = plan->theta;
+    cp.w_step = plan->w_step;
+    cp.shear_u = plan->shear_u;
+    cp.shear_v = plan->shear_v;
+    cp.pswf_lm = plan->d_pswf_lm;
+    cp.pswf_n = plan->d_pswf_n;
+    cp.n_pswf_n = plan->n_pswf_n;
+    cp.c_n = plan->w_support * (M_PI / 2);
+    cp.w_offset = w_offset;
+    cp.inverse = inverse ? 1 : 0;
+    return cp;
+}
+
+} // namespace sdp_wt
 
 extern "C" {
 
@@ -797,7 +734,7 @@ void sdp_gridder_wtower_uvw_degrid(sdp_GridderWtowerUVW* plan,
         SDP_LOG_ERROR("Unsupported image data type");
         return;
     }
-    ensure_device(plan, status);
+    plan_ensure_device(plan, status);
     Staged sg, uv, s, e, v;
     sg.init(subgrid_image, status);
     uv.init(uvws, status);
@@ -852,7 +789,7 @@ void sdp_gridder_wtower_uvw_grid(sdp_GridderWtowerUVW* plan,
                 sdp_mem_type_name(sdp_mem_type(vis)));
         return;
     }
-    ensure_device(plan, status);
+    plan_ensure_device(plan, status);
     Staged sg, uv, s, e, v;
     sg.init(subgrid_image, status);
     uv.init(uvws, status);

@@ -1,0 +1,129 @@
+// The w-towers plan (sdp_GridderWtowerUVW) as shared by the sub-grid
+// gridder (sdp_gridder_wtower_uvw.hip) and the w-stacking driver
+// (sdp_grid_wstack_wtower.hip), and the grid-correction arithmetic.
+#ifndef SDP_WTOWER_PLAN_H_
+#define SDP_WTOWER_PLAN_H_
+
+#include <vector>
+
+#include "ska-sdp-func/grid_data/sdp_gridder_wtower_uvw.h"
+#include "wtower_dev.h"
+#include "../fft/fft2d.h"
+
+struct sdp_GridderWtowerUVW
+{
+    int image_size;
+    int subgrid_size;
+    double theta;
+    double w_step;
+    double shear_u;
+    double shear_v;
+    int support;
+    int oversampling;
+    int w_support;
+    int w_oversampling;
+    int num_w_planes[2];
+    std::vector<double>* uv_kernel;
+    std::vector<double>* w_kernel;
+    std::vector<double>* w_pattern;       // interleaved complex double
+    // Device copies (created on first use).
+    double* d_uv_kernel;
+    double* d_w_kernel;
+    double* d_w_pattern;
+    // Grid-correction tables (created on first use).
+    double* d_pswf_lm;                    // [image_size]
+    double* d_pswf_n;                     // Legendre coefficients
+    int n_pswf_n;
+    // Per-precision scratch: stack [w_support, S, S], w image, FFT buffer.
+    void* d_scratch[2];
+    sdp_fft::Plan2D* fft[2];
+};
+
+namespace sdp_wt {
+
+// Kernel tables and w-pattern on the device (created once per plan).
+void plan_ensure_device(sdp_GridderWtowerUVW* plan, sdp_Error* status);
+
+// PSWF tables of the grid correction on the device.
+void plan_ensure_correction(sdp_GridderWtowerUVW* plan, sdp_Error* status);
+
+// Everything the correction of one pixel needs.
+struct CorrParams
+{
+    int image_size;
+    double theta, w_step, shear_u, shear_v;
+    const double* pswf_lm;    // [image_size]
+    const double* pswf_n;     // Legendre coefficients of pswf_n
+    int n_pswf_n;
+    double c_n;
+    int w_offset;
+    int inverse;              // grid_correct (1) or degrid_correct (0)
+};
+
+CorrParams corr_params(const sdp_GridderWtowerUVW* plan, int w_offset,
+        bool inverse);
+
+// Pixel (pl, pm) relative to the image centre of a facet of element kind
+// `kind` (AnyView): 1 / (pswf(l) pswf(m) pswf_n(n)), then, for complex
+// facets, the w-stacking phasor exp(+-2 pi i w_step n w_offset)
+// (sdp_gridder_grid_correct.cpp:18-116), in the facet's precision.
+// Pixels outside the image (undefined in the reference) are unchanged.
+__device__ __forceinline__ Cx<double> correct_value(Cx<double> z, int kind,
+        int pl, int pm, const CorrParams& cp)
+{
+#pragma clang fp contract(off)
+    const int half = cp.image_size / 2;
+    if (pl + half < 0 || pl + half >= cp.image_size || pm + half < 0 ||
+            pm + half >= cp.image_size)
+        return z;
+    const double l = pl * cp.theta / cp.image_size;
+    const double m = pm * cp.theta / cp.image_size;
+    const double p_l = cp.pswf_lm[pl + half];
+    const double p_m = cp.pswf_lm[pm + half];
+    double p_n = 1.0;
+    const double n = lm_to_n_dev(l, m, cp.shear_u, cp.shear_v);
+    if (cp.c_n > 0.0)
+    {
+        const double n_x = fabs(n * 2.0 * cp.w_step);
+        p_n = (n_x < 1.0) ? pswf_eval(cp.pswf_n, cp.n_pswf_n, n_x) : 1.0;
+    }
+    const double scale = 1.0 / (p_l * p_m * p_n);
+    if (kind <= 1)
+    {
+        z.re *= (kind == 0) ? (double)(float)scale : scale;
+        return z;
+    }
+    if (kind == 2)
+    {
+        const float s = (float)scale;
+        z.re = (double)((float)z.re * s);
+        z.im = (double)((float)z.im * s);
+    }
+    else
+    {
+        z.re *= scale;
+        z.im *= scale;
+    }
+    if (cp.w_offset != 0)
+    {
+        const double phase = 2.0 * M_PI * cp.w_step * n * cp.w_offset;
+        Cx<double> w = cx<double>(cos(phase), sin(phase));
+        if (!cp.inverse) w = cdiv(cx<double>(1.0, 0.0), w);
+        if (kind == 2)
+        {
+            const float wr = (float)w.re, wi = (float)w.im;
+            const float zr = (float)z.re, zi = (float)z.im;
+            z.re = zr * wr - zi * wi;
+            z.im = zr * wi + zi * wr;
+        }
+        else
+        {
+            z = cmul(z, w);
+        }
+    }
+    return z;
+}
+
+} // namespace sdp_wt
+
+#endif

@@ -14,6 +14,12 @@ from .gridder_utils import (
     subgrid_cut_out,
     uvw_bounds_all,
 )
+from .grid_wstack_wtower import (
+    wstack_wtower_degrid_all,
+    wstack_wtower_degrid_planes,
+    wstack_wtower_grid_all,
+    wstack_wtower_grid_planes,
+)
 from .gridder_uvw_es_fft import GridderUvwEsFft
 from .gridder_wtower_uvw import GridderWtowerUVW
 
@@ -32,4 +38,8 @@ __all__ = [
     "subgrid_add",
     "subgrid_cut_out",
     "uvw_bounds_all",
+    "wstack_wtower_degrid_all",
+    "wstack_wtower_degrid_planes",
+    "wstack_wtower_grid_all",
+    "wstack_wtower_grid_planes",
 ]

@@ -1,0 +1,186 @@
+"""GPU parity of the w-stacking x w-towers driver
+(csrc/grid_data/sdp_grid_wstack_wtower.hip) with the oracle's restatement
+of sdp_grid_wstack_wtower.cpp (one thread, task by task).
+
+Pins: degridding matches the direct Fourier sum to the kernel accuracy;
+gridding is the exact adjoint of degridding (for image pixels away from
+the PSWF's 1e-15 end value); shards of w-stack planes sum to the whole.
+Tolerances: complex128 results agree with the oracle to 2e-9 of the
+largest value (summation order, FFT library, and the common w-layer range
+of a batch of sub-grids, which changes the number of w-pattern divisions
+but not the result), complex64 to 5e-5. Image comparisons
+skip a 32-pixel border, where the grid correction divides by the PSWF's
+near-zero tail and amplifies rounding by up to 1e8 (the reference's own
+full-image test skips 30 pixels, test_gridder_wtower_uvw.py:2189-2193).
+"""
+import numpy as np
+import pytest
+
+import wtower_data as wd
+from oracle import wtower_oracle as wo
+
+pytestmark = pytest.mark.gpu
+
+KW = dict(support=8, oversampling=16384, w_support=8, w_oversampling=16384)
+
+
+def _args(case, S):
+    return (case["f0"], case["df"], case["uvw"], S, case["theta"],
+            case["w_step"], 0.0, 0.0, KW["support"], KW["oversampling"],
+            KW["w_support"], KW["w_oversampling"], 0.0, case["H"])
+
+
+def _close(a, b, tol, border=0):
+    if border:
+        a = a[border:-border, border:-border]
+        b = b[border:-border, border:-border]
+    err = np.abs(a - b).max() / max(np.abs(b).max(), 1e-300)
+    assert err <= tol, f"max rel err {err:.3e} > {tol:.1e}"
+
+
+def _image(N, rng, complex_=True):
+    img = rng.normal(size=(N, N))
+    if complex_:
+        img = img + 1j * rng.normal(size=(N, N))
+    return img
+
+
+@pytest.fixture(scope="module")
+def case():
+    return wd.wstack_case(num_rows=1000, num_chan=3)
+
+
+@pytest.mark.parametrize("vis_t,uvw_t,tol", [
+    (np.complex128, np.float64, 2e-9),
+    (np.complex64, np.float32, 5e-5),
+])
+def test_degrid_all_matches_oracle(device, case, vis_t, uvw_t, tol):
+    import ska_sdp_func.grid_data as g
+    rng = np.random.default_rng(1)
+    N, S = 256, 64
+    img = _image(N, rng)
+    # Zero border: the degrid correction amplifies the edge by up to
+    # 1 / pswf(x)^2 (1.5e5 at 16 pixels from the edge here), which single
+    # precision cannot carry; 64 pixels keeps it below 25.
+    bd = 16 if vis_t is np.complex128 else 64
+    img[:bd] = 0
+    img[-bd:] = 0
+    img[:, :bd] = 0
+    img[:, -bd:] = 0
+    uvw = case["uvw"].astype(uvw_t)
+    a = (case["f0"], case["df"], uvw.astype(np.float64)) + _args(case, S)[3:]
+    ref = wo.wstack_degrid_all(img, *a, np.zeros((1000, 3), complex))
+    vis = np.full((1000, 3), 7.0 + 1j, vis_t)          # overwritten
+    image_in = img.astype(np.complex128 if vis_t is np.complex128
+                          else np.complex64)
+    g.wstack_wtower_degrid_all(image_in, a[0], a[1], uvw, *a[3:], 0, vis)
+    _close(vis, ref, tol)
+
+
+@pytest.mark.parametrize("vis_t,uvw_t,img_t,tol", [
+    (np.complex128, np.float64, np.complex128, 2e-9),
+    (np.complex128, np.float64, np.float64, 2e-9),
+    (np.complex64, np.float64, np.float32, 5e-5),
+])
+def test_grid_all_matches_oracle(device, case, vis_t, uvw_t, img_t, tol):
+    import ska_sdp_func.grid_data as g
+    rng = np.random.default_rng(2)
+    N, S = 256, 64
+    vis = (rng.normal(size=(1000, 3)) + 1j * rng.normal(size=(1000, 3)))
+    uvw = case["uvw"].astype(uvw_t)
+    a = (case["f0"], case["df"], uvw.astype(np.float64)) + _args(case, S)[3:]
+    ref = wo.wstack_grid_all(vis, *a, np.zeros((N, N), img_t))
+    out = np.full((N, N), 3.0, img_t)                   # overwritten
+    g.wstack_wtower_grid_all(vis.astype(vis_t), a[0], a[1], uvw, *a[3:], 0,
+                             out)
+    # Single precision: the correction's amplification of rounding near the
+    # edge needs a wider border.
+    _close(out, ref, tol, border=32 if vis_t is np.complex128 else 64)
+
+
+def test_degrid_all_matches_dft(device):
+    """Point sources, 20 000 rows x 4 channels, 512^2: rms error vs the DFT
+    below 1e-4 of the flux (the reference's C test allows 1e-3)."""
+    import ska_sdp_func.grid_data as g
+    N, S = 512, 128
+    c = wd.wstack_case(num_rows=20000, num_chan=4, image_size=N, seed=3,
+                       w_tower_height=8.0, w_planes=4.0)
+    img = np.zeros((N, N))
+    src = [(40, -60, 1.0), (-100, 20, 0.7), (10, 120, 0.4)]
+    for il, im, f in src:
+        img[N // 2 + il, N // 2 + im] = f
+    vis = np.zeros((20000, 4), np.complex128)
+    g.wstack_wtower_degrid_all(img, *_args(c, S)[:2], c["uvw"],
+                               *_args(c, S)[3:], 0, vis)
+    freqs = c["f0"] + np.arange(4) * c["df"]
+    ref = np.zeros_like(vis)
+    for il, im, f in src:
+        l, m = il * c["theta"] / N, im * c["theta"] / N
+        n = wo.lm_to_n(l, m, 0.0, 0.0)
+        ph = (c["uvw"] @ np.array([l, m, n]))[:, None] * (freqs / wd.C_0)
+        ref += f * np.exp(-2j * np.pi * ph)
+    err = np.abs(vis - ref)
+    # A visibility within 1 / (2 w_oversampling) of the top of a w-layer
+    # rounds to the w-kernel row of the layer's bottom (iw0_ov % w_os = 0,
+    # sdp_gridder_wtower_uvw.cpp:127-138, no carry into the next layer) and
+    # comes out a full w_step off; the reference does the same (the oracle
+    # reproduces it exactly). About 1 in 10^4 visibilities; excluded here.
+    ok = err < 1e-3
+    assert np.count_nonzero(~ok) <= err.size // 5000
+    assert np.sqrt(np.mean(err[ok] ** 2)) < 1e-4
+    assert np.count_nonzero(vis) == vis.size
+
+
+def test_grid_all_is_adjoint_and_shards_sum(device):
+    import torch
+    import ska_sdp_func.grid_data as g
+    N, S, R, C = 1024, 128, 100000, 2
+    c = wd.wstack_case(num_rows=R, num_chan=C, image_size=N, seed=4,
+                       w_tower_height=8.0, w_planes=5.0)
+    rng = np.random.default_rng(5)
+    x = _image(N, rng)
+    x[:N // 8] = 0
+    x[-N // 8:] = 0
+    x[:, :N // 8] = 0
+    x[:, -N // 8:] = 0
+    y = rng.normal(size=(R, C)) + 1j * rng.normal(size=(R, C))
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    a = _args(c, S)
+    d_uvw = dev(c["uvw"])
+    ax = torch.zeros((R, C), dtype=torch.complex128, device=device)
+    g.wstack_wtower_degrid_all(dev(x), a[0], a[1], d_uvw, *a[3:], 0, ax)
+    gy = torch.zeros((N, N), dtype=torch.complex128, device=device)
+    g.wstack_wtower_grid_all(dev(y), a[0], a[1], d_uvw, *a[3:], 0, gy)
+    lhs = np.vdot(y, ax.cpu().numpy())
+    rhs = np.vdot(gy.cpu().numpy(), x)
+    assert abs(lhs - rhs) <= 1e-10 * abs(lhs)
+    # Shards of w-stack planes sum to the whole.
+    acc = torch.zeros_like(gy)
+    vacc = torch.zeros_like(ax)
+    for k in range(3):
+        part = torch.zeros_like(gy)
+        g.wstack_wtower_grid_planes(dev(y), a[0], a[1], d_uvw, *a[3:], 0,
+                                    part, k, 3)
+        acc += part
+        vpart = torch.zeros_like(ax)
+        g.wstack_wtower_degrid_planes(dev(x), a[0], a[1], d_uvw, *a[3:], 0,
+                                      vpart, k, 3)
+        vacc += vpart
+    _close(acc.cpu().numpy(), gy.cpu().numpy(), 1e-10, border=128)
+    _close(vacc.cpu().numpy(), ax.cpu().numpy(), 1e-12)
+
+
+def test_argument_errors(device, case):
+    import ska_sdp_func.grid_data as g
+    from ska_sdp_func.utility import CError
+    a = list(_args(case, 64))
+    vis = np.zeros((1000, 3), np.complex128)
+    img = np.zeros((256, 256), np.complex128)
+    a[-1] = 0.0
+    with pytest.raises(CError, match="Invalid function argument"):
+        g.wstack_wtower_grid_all(vis, *a[:2], case["uvw"], *a[3:], 0, img)
+    import torch
+    a[-1] = case["H"]
+    with pytest.raises(CError, match="Memory location"):
+        g.wstack_wtower_grid_all(vis, *a[:2], torch.from_numpy(
+            case["uvw"]).to(device), *a[3:], 0, img)
