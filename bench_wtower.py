@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Benchmark of the w-stacking x w-towers imaging driver at SURVEY.md
+section 8(d) config 4: 10M rows x 1 channel, image 16384^2, sub-grid 256,
+W = W_w = 8, oversampling 16384, subgrid_frac 2/3, w_tower_height from
+determine_max_w_tower_height, w spread over 32 w-stack planes.
+
+A "step" is one wstack_wtower_grid_all over all rows. With --gpus N (one
+process per GPU, torchrun), the w-stack planes are sharded across the ranks
+(grid_planes with plane_offset = rank, plane_stride = N) and the rank
+images are summed on rank 0 with one RCCL reduce inside the timed region;
+total work is fixed ("scaling": "strong"). Inputs are generated in HBM
+(uvw f32, vis c64, f0 = c so that metres are wavelengths).
+
+Prints one JSON line (same field layout as bench.py).
+
+  python bench_wtower.py [--rows 10000000 --image 16384 --steps 3]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ska-sdp-func_amd"))
+sys.path.insert(0, ROOT)
+
+C_0 = 299792458.0
+HBM_PEAK_GBS = 8000.0
+KW = dict(support=8, oversampling=16384, w_support=8, w_oversampling=16384)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--chan", type=int, default=1)
+    ap.add_argument("--image", type=int, default=16384)
+    ap.add_argument("--subgrid", type=int, default=256)
+    ap.add_argument("--planes", type=int, default=32)
+    ap.add_argument("--theta", type=float, default=0.04)
+    ap.add_argument("--degrid", action="store_true")
+    ap.add_argument("--verbosity", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-subgrids", type=int, default=6)
+    return ap.parse_args()
+
+
+def geometry(args):
+    """theta, fov, w_step, w_tower_height (the reference's C test recipe,
+    test_gridder_wtower_uvw.cpp:437-452)."""
+    import ska_sdp_func.grid_data as g
+    theta = args.theta
+    fov = 0.8 * theta
+    w_step = g.determine_w_step(theta, fov, 0.0, 0.0)
+    H = g.determine_max_w_tower_height(
+        args.subgrid, theta, fov, w_step, KW["support"], KW["oversampling"],
+        KW["w_support"], KW["w_oversampling"], image_size=2 * args.subgrid,
+        subgrid_frac=2.0 / 3.0)
+    return theta, fov, w_step, float(H)
+
+
+def make_inputs(torch, dev, args, w_stack_dist, seed):
+    """(u, v) uniform in a disk reaching 0.45 of the grid half-width at the
+    top channel; w uniform over exactly args.planes w-stack planes."""
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    R = args.rows
+    f_max = 1.0 + (args.chan - 1) / 200.0
+    r_max = 0.45 * args.image / args.theta / f_max
+    r = r_max * torch.sqrt(torch.rand(R, generator=gen, device=dev,
+                                      dtype=torch.float64))
+    ph = 2 * math.pi * torch.rand(R, generator=gen, device=dev,
+                                  dtype=torch.float64)
+    half = args.planes / 2
+    w = (torch.rand(R, generator=gen, device=dev, dtype=torch.float64)
+         * args.planes - half - 0.5) * w_stack_dist
+    uvw = torch.stack([r * torch.cos(ph), r * torch.sin(ph), w], dim=1)
+    uvw = uvw.to(torch.float32).contiguous()
+    vis = torch.complex(
+        torch.randn((R, args.chan), generator=gen, device=dev),
+        torch.randn((R, args.chan), generator=gen, device=dev)).contiguous()
+    return uvw, vis
+
+
+def cpu_baseline(uvw_dev, vis_dev, args, theta, w_step, H):
+    """Oracle (oracle/wtower_oracle.py, numpy) on a bounded sample: the
+    sub-grid towers (w-towers gridding + sub-grid FFT) of a few sub-grids
+    of the central w-stack plane; the per-plane image FFT / correction are
+    not in the sample."""
+    import numpy as np
+    from oracle import wtower_oracle as wo
+    uvw = uvw_dev.cpu().numpy().astype(np.float64)
+    vis = vis_dev.cpu().numpy().astype(np.complex128)
+    R, C = vis.shape
+    S = args.subgrid
+    eff = int(math.floor(S * 2.0 / 3.0))
+    eff_dist = eff / theta
+    ws_dist = H * w_step
+    s0 = np.zeros(R, np.int64)
+    e0 = np.full(R, C, np.int64)
+    sw, ew = wo.clamp_rows_vec(uvw[:, 2], C_0, C_0 / 200, s0, e0,
+                               -ws_dist / 2, ws_dist / 2)
+    plan = wo.WtowerPlan(args.image, S, theta, w_step, 0.0, 0.0,
+                         KW["support"], KW["oversampling"], KW["w_support"],
+                         KW["w_oversampling"])
+    n_vis, dt, done = 0, 0.0, 0
+    for iu, iv in [(0, 0), (1, 0), (0, 1), (-1, 0), (0, -1), (1, 1),
+                   (-1, -1), (2, 0)][:args.cpu_sample_subgrids]:
+        su, eu = wo._uv_clamp(uvw, C_0, C_0 / 200, sw, ew, iu, iv, eff_dist)
+        rows = np.nonzero(eu > su)[0]
+        if len(rows) == 0:
+            continue
+        sub = np.zeros((S, S), complex)
+        t0 = time.perf_counter()
+        plan.grid(vis[rows], uvw[rows], su[rows], eu[rows], C_0, C_0 / 200,
+                  sub, iu * eff, iv * eff, 0)
+        wo.fft_shift(sub, True)
+        dt += time.perf_counter() - t0
+        n_vis += int(np.sum(eu[rows] - su[rows]))
+        done += 1
+    return {"value": round(n_vis / dt / 1e6, 6) if dt else None,
+            "unit": "Mvis/s", "cores": 1, "kind": "port",
+            "sample": (f"oracle/wtower_oracle.py (numpy, 1 thread) sub-grid "
+                       f"towers of {done} sub-grids of the central w-stack "
+                       f"plane ({n_vis} vis, {dt:.1f} s); the per-plane "
+                       f"{args.image}^2 FFT and correction are excluded")}
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    import ska_sdp_func.grid_data as g
+
+    theta, fov, w_step, H = geometry(args)
+    uvw, vis = make_inputs(torch, dev, args, H * w_step, 20251015 + 4)
+    N, S = args.image, args.subgrid
+    image = torch.zeros((N, N), dtype=torch.float32, device=dev)
+    common = (C_0, C_0 / 200, uvw, S, theta, w_step, 0.0, 0.0,
+              KW["support"], KW["oversampling"], KW["w_support"],
+              KW["w_oversampling"], 0.0, H)
+
+    def grid_step(verbosity=0):
+        g.wstack_wtower_grid_planes(vis, *common, verbosity, image, rank,
+                                    world)
+        if dist is not None:
+            dist.reduce(image, dst=0)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        grid_step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        grid_step()
+    barrier()
+    t_grid = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([t_grid], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_grid = float(t.item())
+    total_vis = args.rows * args.chan
+    value = total_vis * args.steps / t_grid / 1e6
+    if args.verbosity:
+        grid_step(args.verbosity)
+        barrier()
+
+    degrid = None
+    if args.degrid:
+        out = torch.zeros_like(vis)
+        for _ in range(args.warmup):
+            g.wstack_wtower_degrid_planes(image, *common, 0, out, rank,
+                                          world)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            g.wstack_wtower_degrid_planes(image, *common, 0, out, rank,
+                                          world)
+        barrier()
+        t_deg = time.perf_counter() - t0
+        degrid = {"mvis_s": round(total_vis * args.steps / t_deg / 1e6, 3),
+                  "ms_per_step": round(1e3 * t_deg / args.steps, 2)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(uvw, vis, args, theta, w_step, H)
+        except Exception as exc:  # baseline failure must not hide the bench
+            cpu = {"value": None, "unit": "Mvis/s", "cores": 1,
+                   "kind": "port", "sample": f"failed: {exc!r}"}
+
+    if rank == 0:
+        line = {
+            "metric": "Mvis/s gridded",
+            "value": round(value, 3),
+            "unit": "Mvis/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * t_grid / args.steps, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (config-4 distribution, generated in HBM)",
+            "config": {
+                "workload": (f"wstack_wtower_grid_all, {args.rows} rows x "
+                             f"{args.chan} chan, image {N}^2, sub-grid {S},"
+                             f" W = W_w = 8, os 16384, {args.planes} w-stack "
+                             f"planes (sharded over {world} GPU(s))"),
+                "theta": theta, "fov": fov, "w_step": w_step,
+                "w_tower_height": H,
+                "parallelism": f"w-stack planes / {world}",
+            },
+            "degrid": degrid,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
