@@ -23,9 +23,14 @@ A restatement (float64 / complex128 throughout) of ska-sdp-func 1.2.2:
   sdp_grid_wstack_wtower.cpp    grid_all :467-700, degrid_all :218-448
 Used only by tests/ as the checker of the HIP implementation.
 
-Parity status: the reference's CPU path could not be run here (DESIGN.md,
-"Denied"); absolute values are pinned by the DFT (the gridder must reproduce
-a direct Fourier sum to its kernel accuracy) and the PSWF values by scipy.
+Parity status: PARITY UNPINNED against reference outputs. The reference
+holds no golden vectors or fixtures for this path (its tests compare the
+C++ against an in-file NumPy model), and running or importing reference
+code here was refused ("Denied"). The restatement is instead
+cross-checked by identities the reference algorithm must satisfy: degridding
+reproduces the direct Fourier sum to the PSWF kernels' accuracy, gridding
+is the exact adjoint of degridding, and the PSWF values agree with
+scipy.special.pro_ang1 (the Zhang & Jin algorithm the reference ports).
 """
 import math
 

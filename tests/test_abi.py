@@ -185,47 +185,6 @@ def test_get_w_range_numpy():
     assert GridderUvwEsFft.get_w_range([1, 2], freq) == (-1, -1)
 
 
-REF_SRC = "/root/reference/src"
-
-
-@pytest.mark.skipif(not os.path.isdir(os.path.join(REF_SRC, "ska_sdp_func")),
-                    reason="reference package not present (GPU box)")
-def test_reference_python_wrapper_binds_this_library(tmp_path):
-    """The reference's OWN ska_sdp_func package (unmodified, read-only) loads
-    this libska_sdp_func.so via SKA_SDP_FUNC_LIB_DIR and gets the same
-    status codes -- the drop-in claim at the ctypes boundary. Runs in a
-    subprocess so the two packages of the same name never meet."""
-    code = r"""
-import numpy as np
-from ska_sdp_func.grid_data import GridderUvwEsFft
-from ska_sdp_func.utility import CError, Lib
-assert Lib.find_lib(list(Lib.search_dirs)).startswith(%r)
-uvw = np.zeros((100, 3)); f = 1e9 + np.arange(10) * 1e8
-v = np.zeros((100, 10), complex); w = np.ones((100, 10)); d = np.zeros((64, 64))
-out = []
-for a in [(uvw.astype(complex), f, v, w, d), (uvw, f, v.astype(np.complex64), w, d),
-          (np.ascontiguousarray(uvw[:, :2]), f, v, w, d), (uvw, f, v, w, d)]:
-    try:
-        g = GridderUvwEsFft(*a, 1e-4, 1e-4, 1e-5, False)
-        g.grid_uvw_es_fft(*a)
-        out.append("ok")
-    except CError as e:
-        out.append(str(e))
-print("|".join(out))
-""" % (os.path.dirname(LIB),)
-    env = dict(os.environ, SKA_SDP_FUNC_LIB_DIR=os.path.dirname(LIB),
-               PYTHONPATH=REF_SRC, PYTHONDONTWRITEBYTECODE="1")
-    res = subprocess.run([os.sys.executable, "-c", code], env=env,
-                         cwd=str(tmp_path), capture_output=True, text=True,
-                         timeout=300)
-    assert res.returncode == 0, res.stderr[-2000:]
-    assert res.stdout.strip().splitlines()[-1] == "|".join([
-        "Error 3: Unsupported data type(s)",
-        "Error 3: Unsupported data type(s)",
-        "Error 2: Invalid function argument",
-        "Error 6: Memory location mismatch"])
-
-
 # Flagger argument checks (sdp_flagger.cpp:10-57): all raised before any
 # device work, so they run without a GPU.
 def _flag_call(vis, flags, **over):
