@@ -23,7 +23,9 @@ PHASES = {
     "tile_kernel": ("k_scatter_mfma", "k_scatter<", "k_scatter(",
                     "k_gather_mfma", "k_gather<", "k_gather("),
     "image": ("k_screen_corr_2d", "k_screen_accumulate", "k_apply_correction",
-              "k_reverse_screen"),
+              "k_reverse_screen", "k_cols_b_grid"),
+    # fused FFT passes (es_fft.hip); rocFFT kernels match "fft" below
+    "fft": ("k_rows_grid", "k_cols_a_grid"),
 }
 
 
