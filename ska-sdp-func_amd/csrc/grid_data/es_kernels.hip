@@ -873,6 +873,274 @@ __global__ __launch_bounds__(256) void k_scatter_mfma(EsParams<float> p,
     }
 }
 
+// Atomic-free visit pool of one chunk (tap-table kernels). Phase 1, before
+// a barrier: each wave ballots its entries per sub-tile, keeps for every
+// hit the entry's rank inside the ballot, and lane st publishes the wave's
+// count for sub-tile st. Phase 2, after it: every wave derives the pool
+// layout itself (sub-tile-major, wave-minor) with a 32-lane scan, so no
+// LDS atomics and no serial prefix stand between the barriers.
+template<int kNS>
+struct PoolCounts
+{
+    uint32_t c[4][kNS];
+};
+
+template<int kSub>
+__device__ __forceinline__ void pool_count(PoolCounts<kSub * kSub>& pc,
+        int lane, int wave, int wlo_r, int whi_r, int wlo_c, int whi_c,
+        int sub[4], int rank[4])
+{
+    int nh = 0;
+    uint32_t my_cnt = 0;
+#pragma unroll
+    for (int st = 0; st < kSub * kSub; ++st)
+    {
+        const int sr = st / kSub, sc = st % kSub;
+        const bool hit = sr >= wlo_r && sr <= whi_r && sc >= wlo_c &&
+                sc <= whi_c;
+        const uint64_t m = __ballot(hit);
+        if (lane == st) my_cnt = (uint32_t)__popcll(m);
+        if (hit && nh < 4)
+        {
+            sub[nh] = st;
+            rank[nh] = (int)__popcll(m & ((1ull << lane) - 1ull));
+            ++nh;
+        }
+    }
+    for (int k = nh; k < 4; ++k) sub[k] = -1;
+    if (lane < kSub * kSub) pc.c[wave][lane] = my_cnt;
+}
+
+// Lane L < kNS receives sub-tile L's pool begin and size, and the begin
+// of this wave's part of it.
+template<int kNS>
+__device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
+        int lane, int wave, int& beg, int& tot, int& base)
+{
+    int t = 0, pre = 0;
+    if (lane < kNS)
+    {
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+        {
+            const int c = (int)pc.c[w][lane];
+            t += c;
+            pre += (w < wave) ? c : 0;
+        }
+    }
+    int incl = t;
+#pragma unroll
+    for (int d = 1; d < 32; d *= 2)
+    {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    beg = incl - t;
+    tot = t;
+    base = beg + pre;
+}
+
+// Grid mode, f32, matrix-core form with per-entry tap tables (the hot path
+// for W <= 16). Same tile / sub-tile / accumulator organisation as
+// k_scatter_mfma, but the ES taps are evaluated ONCE per bucketed entry
+// instead of once per (entry, sub-tile) visit and lane: at staging, thread
+// t evaluates the NTAP u-taps (checkerboard sign folded in) and the NTAP
+// v-taps times the weighted visibility of its entry into LDS tables
+// (identical arithmetic to k_scatter_mfma, so the products fed to the
+// matrix core are bit-identical). A visit is a packed 32-bit
+// {entry, u0 - tile row + 32, v0 - tile col + 32} word. Per chunk: the
+// next chunk's records are prefetched, the pool is laid out without
+// atomics (pool_count / pool_layout), three barriers, and the MFMA loop
+// issues all LDS reads of four groups before the matrix ops.
+template<bool DO_W, int NTAP>
+__global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
+        const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
+        const uint32_t* __restrict__ item_start,
+        const uint32_t* __restrict__ item_bin, float* __restrict__ grid)
+{
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int kChunk = 256;           // one entry per thread
+    constexpr int kVec = DO_W ? 2 : 1;    // float4s per bucketed record
+    __shared__ uint32_t s_pool[4 * kChunk];   // packed visits
+    // Tap tables; the extra last element of each is a zero that masked
+    // lanes read instead of branching around the load.
+    constexpr int kZero = kChunk * NTAP;
+    __shared__ float s_ku[kChunk * NTAP + 1];     // signed u-taps per entry
+    __shared__ float2 s_kv[kChunk * NTAP + 1];    // signed v-taps x w V
+    __shared__ PoolCounts<16> s_pc;
+
+    const uint32_t item = blockIdx.x;
+    if (item_bin[item] == kNoBin) return;   // past the last work item
+    const int b = (int)item_bin[item];
+    const uint32_t piece = item - item_start[b];
+    const uint32_t npieces = item_start[b + 1] - item_start[b];
+    const uint32_t e0 = bin_start[b] + piece * kPiece;
+    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
+    const int half = p.G / 2;
+    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    const int tu0 = r0 - half, tv0 = c0 - half;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int i = lane & 15, kq = lane >> 4;
+    const int sub_r = wave * 16;           // this wave's row band
+    const int base_u = sub_r + i + 32;     // tap index = base_u - packed ou
+    const float hs = (float)p.support / 2.0f;
+    const float inv_hs = 1.0f / hs;
+    f32x4 acc_re[4], acc_im[4];
+#pragma unroll
+    for (int cblk = 0; cblk < 4; ++cblk)
+    {
+        acc_re[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        acc_im[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    if (t == 0)
+    {
+        s_ku[kZero] = 0.0f;
+        s_kv[kZero] = make_float2(0.0f, 0.0f);
+    }
+    const float4* recs4 = (const float4*)recs;
+    float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rw = r;
+    if (e0 + t < e1)
+    {
+        r = recs4[(size_t)(e0 + t) * kVec];
+        if (DO_W) rw = recs4[(size_t)(e0 + t) * kVec + 1];
+    }
+
+    for (uint32_t cb = e0; cb < e1; cb += kChunk)
+    {
+        const int n = (int)min((uint32_t)kChunk, e1 - cb);
+        float4 rn = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rwn = rn;
+        if (cb + kChunk + t < e1)   // prefetch the next chunk
+        {
+            rn = recs4[(size_t)(cb + kChunk + t) * kVec];
+            if (DO_W) rwn = recs4[(size_t)(cb + kChunk + t) * kVec + 1];
+        }
+        int wlo_r = 1, whi_r = 0, wlo_c = 1, whi_c = 0;
+        int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
+        uint32_t pk = 0;
+        if (t < n)
+        {
+#pragma clang fp contract(off)
+            if (DO_W)
+            {
+                r.z *= rw.x;
+                r.w *= rw.x;
+            }
+            tap_range(p, r.x, r.y, u0, u1, v0, v1);
+            wlo_r = max(u0 - tu0, 0) >> 4;
+            whi_r = min(u1 - tu0, kTile - 1) >> 4;
+            wlo_c = max(v0 - tv0, 0) >> 4;
+            whi_c = min(v1 - tv0, kTile - 1) >> 4;
+            pk = (uint32_t)t | (uint32_t)(u0 - tu0 + 32) << 8 |
+                    (uint32_t)(v0 - tv0 + 32) << 16;
+        }
+        int sub[4], rank[4];
+        pool_count<4>(s_pc, lane, wave, wlo_r, whi_r, wlo_c, whi_c, sub,
+                rank);
+        __syncthreads();   // B1: previous chunk's tables consumed
+        if (t < n)
+        {
+#pragma clang fp contract(off)
+#pragma unroll
+            for (int d = 0; d < NTAP; ++d)
+            {
+                const int u = u0 + d, v = v0 + d;
+                const float ka = es_tap_fast(p.beta, ((float)u - r.x) * inv_hs);
+                const float kb = es_tap_fast(p.beta, ((float)v - r.y) * inv_hs);
+                const float a = (u & 1) ? -ka : ka;
+                const float kv = (v & 1) ? -kb : kb;
+                s_ku[t * NTAP + d] = (u <= u1) ? a : 0.0f;
+                s_kv[t * NTAP + d] = (v <= v1) ?
+                        make_float2(kv * r.z, kv * r.w) :
+                        make_float2(0.0f, 0.0f);
+            }
+        }
+        __syncthreads();   // B2: counts and tap tables complete
+        int beg_l, tot_l, base_l;
+        pool_layout<16>(s_pc, lane, wave, beg_l, tot_l, base_l);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+        {
+            const int pos = __shfl(base_l, max(sub[k], 0), 64) + rank[k];
+            if (sub[k] >= 0) s_pool[pos] = pk;
+        }
+        __syncthreads();   // B3: pool complete
+#pragma unroll
+        for (int cblk = 0; cblk < 4; ++cblk)
+        {
+            const int st = __builtin_amdgcn_readfirstlane(wave * 4 + cblk);
+            const int v_beg = __builtin_amdgcn_readlane(beg_l, st);
+            const int cnt = __builtin_amdgcn_readlane(tot_l, st);
+            const int base_v = cblk * 16 + i + 32;
+            // Four groups of four visits per step: all LDS reads of a step
+            // are issued before the first matrix op waits on them.
+            for (int g = 0; g < cnt; g += 16)
+            {
+                uint32_t q[4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                    q[s] = s_pool[v_beg + min(g + 4 * s + kq, cnt - 1)];
+                float a[4];
+                float2 bb[4];
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                {
+                    const int e = (int)(q[s] & 0xffu);
+                    const int du = base_u - (int)((q[s] >> 8) & 0xffu);
+                    const int dv = base_v - (int)(q[s] >> 16);
+                    const bool valid = g + 4 * s + kq < cnt;
+                    const int ia = (valid && (unsigned)du < (unsigned)NTAP) ?
+                            e * NTAP + du : kZero;
+                    const int ib = ((unsigned)dv < (unsigned)NTAP) ?
+                            e * NTAP + dv : kZero;
+                    a[s] = s_ku[ia];
+                    bb[s] = s_kv[ib];
+                }
+                // Groups past cnt multiply zeros (a = 0): no branch, so
+                // the loads above stay batched ahead of the matrix ops.
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                {
+                    acc_re[cblk] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s],
+                            bb[s].x, acc_re[cblk], 0, 0, 0);
+                    acc_im[cblk] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s],
+                            bb[s].y, acc_im[cblk], 0, 0, 0);
+                }
+            }
+        }
+        r = rn;
+        rw = rwn;
+    }
+
+    // C/D layout of 16x16x4 f32: col = lane & 15, row = (lane >> 4)*4 + r.
+#pragma unroll
+    for (int cblk = 0; cblk < 4; ++cblk)
+    {
+        const int col = c0 + cblk * 16 + i;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+        {
+            const int row = r0 + sub_r + kq * 4 + rr;
+            if (row >= p.G || col >= p.G) continue;
+            float* dst = grid + ((size_t)row * p.G + col) * 2;
+            if (npieces == 1)
+            {
+                float2 v;
+                v.x = acc_re[cblk][rr];
+                v.y = acc_im[cblk][rr];
+                *(float2*)dst = v;
+            }
+            else
+            {
+                if (acc_re[cblk][rr] != 0.0f)
+                    unsafeAtomicAdd(dst, acc_re[cblk][rr]);
+                if (acc_im[cblk][rr] != 0.0f)
+                    unsafeAtomicAdd(dst + 1, acc_im[cblk][rr]);
+            }
+        }
+    }
+}
+
 // Degrid mode, f32, matrix-core form (the hot path).
 //
 // For visibility j and a 16x16 sub-tile (rows R, cols C) of the grid,
@@ -1026,6 +1294,187 @@ __global__ __launch_bounds__(256) void k_gather_mfma(EsParams<float> p,
             vis[2 * idx] += s_acc_re[t];
             vis[2 * idx + 1] += s_acc_im[t] * flip;   // kernels.cu:267-268
         }
+    }
+}
+
+// Degrid mode, f32, matrix-core form with per-entry tap tables (the hot
+// path for W <= 16). Same organisation as k_gather_mfma (5 x 5 sub-tiles
+// of a tile + halo, T = G_sub * Kv on the matrix core, u-taps applied on
+// the lane-group reduction), but each entry's NTAP u-taps and v-taps
+// (checkerboard sign folded in) are evaluated once at staging into LDS
+// tables, with the same arithmetic as k_gather_mfma; visits are packed
+// {entry, u0 - tile row, v0 - tile col} words; the pool is laid out
+// without atomics and the next chunk's records are prefetched.
+template<bool DO_W, int NTAP>
+__global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
+        const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
+        const uint32_t* __restrict__ item_start,
+        const uint32_t* __restrict__ item_bin, const float* __restrict__ grid,
+        float* __restrict__ vis)
+{
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    constexpr int kChunk = 256;
+    constexpr int kSub = 5;                 // 5 x 5 sub-tiles: tile + halo
+    constexpr int kZero = kChunk * NTAP;    // zero element for masked lanes
+    __shared__ uint32_t s_pool[4 * kChunk]; // packed visits
+    __shared__ float s_ku[kChunk * NTAP + 1];
+    __shared__ float s_kv[kChunk * NTAP + 1];
+    __shared__ float s_kw[kChunk];
+    __shared__ float s_acc_re[kChunk];
+    __shared__ float s_acc_im[kChunk];
+    __shared__ PoolCounts<kSub * kSub> s_pc;
+
+    const uint32_t item = blockIdx.x;
+    if (item_bin[item] == kNoBin) return;   // past the last work item
+    const int b = (int)item_bin[item];
+    const uint32_t piece = item - item_start[b];
+    const uint32_t e0 = bin_start[b] + piece * kPiece;
+    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
+    if (e0 >= e1) return;   // empty tile
+    const int half = p.G / 2;
+    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    const int tu0 = r0 - half, tv0 = c0 - half;
+    const float2* g2 = (const float2*)grid;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wave = t >> 6;
+    const int jl = lane & 15, kq = lane >> 4;
+    const float hs = (float)p.support / 2.0f;
+    const float inv_hs = 1.0f / hs;
+    const float4* recs4 = (const float4*)recs;
+    if (t == 0)
+    {
+        s_ku[kZero] = 0.0f;
+        s_kv[kZero] = 0.0f;
+    }
+    float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (e0 + t < e1) r = recs4[e0 + t];
+
+    for (uint32_t cb = e0; cb < e1; cb += kChunk)
+    {
+        const int n = (int)min((uint32_t)kChunk, e1 - cb);
+        float4 rn = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (cb + kChunk + t < e1) rn = recs4[cb + kChunk + t];   // prefetch
+        int wlo_r = 1, whi_r = 0, wlo_c = 1, whi_c = 0;
+        int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
+        uint32_t pk = 0;
+        if (t < n)
+        {
+            tap_range(p, r.x, r.y, u0, u1, v0, v1);
+            wlo_r = (u0 - tu0) >> 4;
+            whi_r = min(u1 - tu0, kSub * 16 - 1) >> 4;
+            wlo_c = (v0 - tv0) >> 4;
+            whi_c = min(v1 - tv0, kSub * 16 - 1) >> 4;
+            pk = (uint32_t)t | (uint32_t)(u0 - tu0) << 8 |
+                    (uint32_t)(v0 - tv0) << 16;
+        }
+        int sub[4], rank[4];
+        pool_count<kSub>(s_pc, lane, wave, wlo_r, whi_r, wlo_c, whi_c, sub,
+                rank);
+        __syncthreads();   // B1: previous chunk consumed
+        if (t < n)
+        {
+#pragma clang fp contract(off)
+#pragma unroll
+            for (int d = 0; d < NTAP; ++d)
+            {
+                const int u = u0 + d, v = v0 + d;
+                const float ka = es_tap_fast(p.beta, ((float)u - r.x) * inv_hs);
+                const float kb = es_tap_fast(p.beta, ((float)v - r.y) * inv_hs);
+                s_ku[t * NTAP + d] = (u <= u1) ? ((u & 1) ? -ka : ka) : 0.0f;
+                s_kv[t * NTAP + d] = (v <= v1) ? ((v & 1) ? -kb : kb) : 0.0f;
+            }
+            s_kw[t] = DO_W ? fabsf(r.z) : 1.0f;
+        }
+        s_acc_re[t] = 0.0f;
+        s_acc_im[t] = 0.0f;
+        __syncthreads();   // B2: counts, tables, accumulators ready
+        int beg_l, tot_l, base_l;
+        pool_layout<kSub * kSub>(s_pc, lane, wave, beg_l, tot_l, base_l);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+        {
+            const int pos = __shfl(base_l, max(sub[k], 0), 64) + rank[k];
+            if (sub[k] >= 0) s_pool[pos] = pk;
+        }
+        __syncthreads();   // B3: pool complete
+        for (int st = wave; st < kSub * kSub; st += 4)
+        {
+            const int sts = __builtin_amdgcn_readfirstlane(st);
+            const int cnt = __builtin_amdgcn_readlane(tot_l, sts);
+            if (cnt == 0) continue;
+            const int v_beg = __builtin_amdgcn_readlane(beg_l, sts);
+            const int R0 = (sts / kSub) * 16, C0 = (sts % kSub) * 16;
+            // A operands straight from the grid (L2 / HBM):
+            // G[r0 + R0 + jl][c0 + C0 + 4 kk + kq], kk = 0..3.
+            float a_re[4], a_im[4];
+            const int grow = r0 + R0 + jl;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+            {
+                const int gcol = c0 + C0 + 4 * kk + kq;
+                float2 v = make_float2(0.0f, 0.0f);
+                if (grow < p.G && gcol < p.G) v = g2[(size_t)grow * p.G + gcol];
+                a_re[kk] = v.x;
+                a_im[kk] = v.y;
+            }
+            for (int g = 0; g < cnt; g += 16)
+            {
+#pragma clang fp contract(off)
+                const bool valid = g + jl < cnt;
+                const uint32_t q = s_pool[v_beg + (valid ? g + jl : cnt - 1)];
+                const int e = (int)(q & 0xffu);
+                const int eb = e * NTAP;
+                const int ou = (int)((q >> 8) & 0xffu), ov = (int)(q >> 16);
+                f32x4 t_re = {0.0f, 0.0f, 0.0f, 0.0f};
+                f32x4 t_im = {0.0f, 0.0f, 0.0f, 0.0f};
+                float kv[4], ku[4];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                {
+                    const int dv = C0 + 4 * kk + kq - ov;
+                    kv[kk] = s_kv[((unsigned)dv < (unsigned)NTAP) ? eb + dv :
+                            kZero];
+                    const int du = R0 + 4 * kq + kk - ou;
+                    ku[kk] = s_ku[(valid && (unsigned)du < (unsigned)NTAP) ?
+                            eb + du : kZero];
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                {
+                    t_re = __builtin_amdgcn_mfma_f32_16x16x4f32(a_re[kk],
+                            kv[kk], t_re, 0, 0, 0);
+                    t_im = __builtin_amdgcn_mfma_f32_16x16x4f32(a_im[kk],
+                            kv[kk], t_im, 0, 0, 0);
+                }
+                float p_re = 0.0f, p_im = 0.0f;
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr)
+                {
+                    p_re += ku[rr] * t_re[rr];
+                    p_im += ku[rr] * t_im[rr];
+                }
+                // Sum the four lane groups (rows 4kq..4kq+3).
+                p_re += __shfl_xor(p_re, 16);
+                p_im += __shfl_xor(p_im, 16);
+                p_re += __shfl_xor(p_re, 32);
+                p_im += __shfl_xor(p_im, 32);
+                if (kq == 0 && valid)
+                {
+                    const float kw = s_kw[e];
+                    atomicAdd(&s_acc_re[e], p_re * kw);
+                    atomicAdd(&s_acc_im[e], p_im * kw);
+                }
+            }
+        }
+        __syncthreads();
+        if (t < n)
+        {
+            const uint64_t idx = (uint64_t)__float_as_uint(r.w);
+            const float flip = signbit(r.z) ? -1.0f : 1.0f;
+            vis[2 * idx] += s_acc_re[t];
+            vis[2 * idx + 1] += s_acc_im[t] * flip;   // kernels.cu:267-268
+        }
+        r = rn;
     }
 }
 
@@ -1375,6 +1824,17 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
     return *status;
 }
 
+// Tap-table tile kernels (k_scatter_tab / k_gather_tab) unless
+// SDP_ES_TAP_TABLES=0 selects the per-visit tap kernels (A/B measurement).
+bool use_tap_tables()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("SDP_ES_TAP_TABLES");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template<typename T>
 int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         T* grid, hipStream_t stream)
@@ -1386,12 +1846,29 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     SDP_HIP_CHECK_LAUNCH(status);
     if constexpr (sizeof(T) == 4)
     {
-        if (p.do_w)
+        const float* recs = (const float*)s.recs;
+        if (!use_tap_tables())
+            ;
+        else if (p.support <= 8 && p.do_w)
+            k_scatter_tab<true, 9><<<n_items, 256, 0, stream>>>(
+                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
+        else if (p.support <= 8)
+            k_scatter_tab<false, 9><<<n_items, 256, 0, stream>>>(
+                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
+        else if (p.support <= 16 && p.do_w)
+            k_scatter_tab<true, 17><<<n_items, 256, 0, stream>>>(
+                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
+        else if (p.support <= 16)
+            k_scatter_tab<false, 17><<<n_items, 256, 0, stream>>>(
+                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
+        if (use_tap_tables() && p.support <= 16)
+            ;
+        else if (p.do_w)
             k_scatter_mfma<true><<<n_items, 256, 0, stream>>>(
-                    p, (const float*)s.recs, s.bin_start, s.item_start, s.item_bin, grid);
+                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
         else
             k_scatter_mfma<false><<<n_items, 256, 0, stream>>>(
-                    p, (const float*)s.recs, s.bin_start, s.item_start, s.item_bin, grid);
+                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
         SDP_HIP_CHECK_LAUNCH(status);
         return *status;
     }
@@ -1420,6 +1897,26 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     sdp_Error* status = &st;
     if constexpr (sizeof(T) == 4)
     {
+        const float* recs = (const float*)s.recs;
+        if (!use_tap_tables())
+            ;
+        else if (p.support <= 8 && p.do_w)
+            k_gather_tab<true, 9><<<n_items, 256, 0, stream>>>(p, recs,
+                    s.bin_start, s.item_start, s.item_bin, grid, vis);
+        else if (p.support <= 8)
+            k_gather_tab<false, 9><<<n_items, 256, 0, stream>>>(p, recs,
+                    s.bin_start, s.item_start, s.item_bin, grid, vis);
+        else if (p.support <= 16 && p.do_w)
+            k_gather_tab<true, 17><<<n_items, 256, 0, stream>>>(p, recs,
+                    s.bin_start, s.item_start, s.item_bin, grid, vis);
+        else if (p.support <= 16)
+            k_gather_tab<false, 17><<<n_items, 256, 0, stream>>>(p, recs,
+                    s.bin_start, s.item_start, s.item_bin, grid, vis);
+        if (p.support <= 16 && use_tap_tables())
+        {
+            SDP_HIP_CHECK_LAUNCH(status);
+            return *status;
+        }
         if (p.support <= 16)
         {
             if (p.do_w)
