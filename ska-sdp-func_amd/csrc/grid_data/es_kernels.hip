@@ -961,13 +961,15 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     constexpr int kChunk = 256;           // one entry per thread
     constexpr int kVec = DO_W ? 2 : 1;    // float4s per bucketed record
-    __shared__ uint32_t s_pool[4 * kChunk];   // packed visits
+    // Per-wave visit lists: wave w, column block c holds the chunk's
+    // entries whose taps touch sub-tile (w, c), in entry order.
+    __shared__ uint16_t s_list[4][4][kChunk];
+    __shared__ uint32_t s_info[kChunk];        // packed entry + hit masks
     // Tap tables; the extra last element of each is a zero that masked
     // lanes read instead of branching around the load.
     constexpr int kZero = kChunk * NTAP;
     __shared__ float s_ku[kChunk * NTAP + 1];     // signed u-taps per entry
     __shared__ float2 s_kv[kChunk * NTAP + 1];    // signed v-taps x w V
-    __shared__ PoolCounts<16> s_pc;
 
     const uint32_t item = blockIdx.x;
     if (item_bin[item] == kNoBin) return;   // past the last work item
@@ -1031,13 +1033,14 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
             whi_r = min(u1 - tu0, kTile - 1) >> 4;
             wlo_c = max(v0 - tv0, 0) >> 4;
             whi_c = min(v1 - tv0, kTile - 1) >> 4;
+            // bits 24-27: row bands hit, 28-31: column blocks hit
+            const uint32_t rm = (2u << whi_r) - (1u << wlo_r);
+            const uint32_t cm = (2u << whi_c) - (1u << wlo_c);
             pk = (uint32_t)t | (uint32_t)(u0 - tu0 + 32) << 8 |
-                    (uint32_t)(v0 - tv0 + 32) << 16;
+                    (uint32_t)(v0 - tv0 + 32) << 16 | rm << 24 | cm << 28;
         }
-        int sub[4], rank[4];
-        pool_count<4>(s_pc, lane, wave, wlo_r, whi_r, wlo_c, whi_c, sub,
-                rank);
         __syncthreads();   // B1: previous chunk's tables consumed
+        s_info[t] = pk;
         if (t < n)
         {
 #pragma clang fp contract(off)
@@ -1055,22 +1058,33 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                         make_float2(0.0f, 0.0f);
             }
         }
-        __syncthreads();   // B2: counts and tap tables complete
-        int beg_l, tot_l, base_l;
-        pool_layout<16>(s_pc, lane, wave, beg_l, tot_l, base_l);
+        __syncthreads();   // B2: entry info and tap tables complete
+        // This wave's visit lists (deterministic: entry order), by ballot
+        // compaction over the chunk's entries.
+        int lcnt[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int gi = 0; gi < 4; ++gi)
         {
-            const int pos = __shfl(base_l, max(sub[k], 0), 64) + rank[k];
-            if (sub[k] >= 0) s_pool[pos] = pk;
+            const uint32_t info = s_info[gi * 64 + lane];
+            const bool in_band = (info >> (24 + wave)) & 1u;
+#pragma unroll
+            for (int cblk = 0; cblk < 4; ++cblk)
+            {
+                const bool hit = in_band && ((info >> (28 + cblk)) & 1u);
+                const uint64_t m = __ballot(hit);
+                const int pos = lcnt[cblk] +
+                        (int)__popcll(m & ((1ull << lane) - 1ull));
+                if (hit) s_list[wave][cblk][pos] = (uint16_t)(info & 0xffu);
+                lcnt[cblk] += (int)__popcll(m);
+            }
         }
-        __syncthreads();   // B3: pool complete
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int cblk = 0; cblk < 4; ++cblk)
         {
-            const int st = __builtin_amdgcn_readfirstlane(wave * 4 + cblk);
-            const int v_beg = __builtin_amdgcn_readlane(beg_l, st);
-            const int cnt = __builtin_amdgcn_readlane(tot_l, st);
+            const int cnt = __builtin_amdgcn_readfirstlane(lcnt[cblk]);
+            const uint16_t* list = s_list[wave][cblk];
             const int base_v = cblk * 16 + i + 32;
             // Four groups of four visits per step: all LDS reads of a step
             // are issued before the first matrix op waits on them.
@@ -1079,7 +1093,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 uint32_t q[4];
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
-                    q[s] = s_pool[v_beg + min(g + 4 * s + kq, cnt - 1)];
+                    q[s] = s_info[list[min(g + 4 * s + kq, cnt - 1)]];
                 float a[4];
                 float2 bb[4];
 #pragma unroll
@@ -1087,7 +1101,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 {
                     const int e = (int)(q[s] & 0xffu);
                     const int du = base_u - (int)((q[s] >> 8) & 0xffu);
-                    const int dv = base_v - (int)(q[s] >> 16);
+                    const int dv = base_v - (int)((q[s] >> 16) & 0xffu);
                     const bool valid = g + 4 * s + kq < cnt;
                     const int ia = (valid && (unsigned)du < (unsigned)NTAP) ?
                             e * NTAP + du : kZero;
