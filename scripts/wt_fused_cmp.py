@@ -1,0 +1,67 @@
+"""Fused (k_tower_dft) vs layer-by-layer w-tower gridding on one config-4
+shaped case: run once per mode (SDP_WT_FUSED=1 / 0 in the environment,
+read once per process), then compare.
+
+  python scripts/wt_fused_cmp.py run OUT.npy [--rows R --image N ...]
+  python scripts/wt_fused_cmp.py cmp A.npy B.npy
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ska-sdp-func_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import numpy as np
+    if sys.argv[1] == "cmp":
+        a, b = np.load(sys.argv[2]), np.load(sys.argv[3])
+        bd = 64
+        ai, bi = a[bd:-bd, bd:-bd], b[bd:-bd, bd:-bd]
+        err = np.abs(ai - bi).max() / np.abs(bi).max()
+        rms = np.sqrt(np.mean(np.abs(ai - bi) ** 2) / np.mean(np.abs(bi) ** 2))
+        print(f"max rel err {err:.3e}, rms rel err {rms:.3e}")
+        print("norms", np.linalg.norm(ai), np.linalg.norm(bi))
+        for name, x in (("T", a.T), ("flipud", a[::-1]), ("fliplr", a[:, ::-1]),
+                        ("rot180", a[::-1, ::-1]), ("neg", -a)):
+            xi = x[bd:-bd, bd:-bd]
+            print(name, np.abs(xi - bi).max() / np.abs(bi).max())
+        assert err < 1e-5, err
+        return
+    import torch
+    import bench_wtower as bw
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode")
+    ap.add_argument("out")
+    ap.add_argument("--rows", type=int, default=300_000)
+    ap.add_argument("--image", type=int, default=4096)
+    ap.add_argument("--subgrid", type=int, default=256)
+    ap.add_argument("--planes", type=int, default=4)
+    ap.add_argument("--theta", type=float, default=0.04)
+    ap.add_argument("--chan", type=int, default=1)
+    ap.add_argument("--verbosity", type=int, default=0)
+    args = ap.parse_args()
+    import ska_sdp_func.grid_data as g
+    dev = torch.device("cuda:0")
+    theta, fov, w_step, H = bw.geometry(args)
+    uvw, vis = bw.make_inputs(torch, dev, args, H * w_step, 7)
+    N, S = args.image, args.subgrid
+    image = torch.zeros((N, N), dtype=torch.float32, device=dev)
+    common = (bw.C_0, bw.C_0 / 200, uvw, S, theta, w_step, 0.0, 0.0,
+              bw.KW["support"], bw.KW["oversampling"], bw.KW["w_support"],
+              bw.KW["w_oversampling"], 0.0, H)
+    g.wstack_wtower_grid_all(vis, *common, args.verbosity, image)
+    torch.cuda.synchronize()
+    image.zero_()
+    t0 = time.perf_counter()
+    g.wstack_wtower_grid_all(vis, *common, 1, image)
+    torch.cuda.synchronize()
+    print(f"{os.environ.get('SDP_WT_FUSED', '1')}: {time.perf_counter() - t0:.3f} s")
+    np.save(args.out, image.cpu().numpy())
+
+
+if __name__ == "__main__":
+    main()

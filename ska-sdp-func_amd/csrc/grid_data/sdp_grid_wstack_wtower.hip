@@ -71,6 +71,7 @@ struct Geo
     int64_t nu, nv, niw, ntask;
     int64_t P0, NP;                  // global w-layer index base and count
     int plane_offset, plane_stride;
+    int fused;                       // sort runs by (group, slot, layer)
 };
 
 // sdp_gridder_clamp_channels_single / _uv row arithmetic
@@ -231,8 +232,11 @@ __global__ void k_bin(const U* __restrict__ uvw, Geo g, BinOut out)
                     if (p_rel < 0 || p_rel >= g.NP) continue;  // (never)
                     if (EMIT)
                     {
-                        const uint64_t key = ((uint64_t)sl.group * g.NP +
-                                p_rel) * out.t_cap + sl.slot;
+                        const uint64_t key = g.fused ?
+                                ((uint64_t)sl.group * out.t_cap + sl.slot) *
+                                g.NP + p_rel :
+                                ((uint64_t)sl.group * g.NP + p_rel) *
+                                out.t_cap + sl.slot;
                         out.keys[pos] = key;
                         out.idx[pos] = (uint32_t)pos;
                         out.items[pos] = make_int4((int)r, (int)sp, (int)ep,
@@ -698,6 +702,325 @@ __global__ void k_image_to_grid(AnyView image, int64_t G,
 }
 
 // ---------------------------------------------------------------------------
+// Fused w-tower gridding for complex-float visibilities (k_tower_dft).
+//
+// The reference moves a w_support-deep stack of S x S sub-grids through
+// every w-layer of a tower with one S x S inverse FFT per layer
+// (sdp_gridder_wtower_uvw.cpp:1024-1113). A layer holds only the taps of
+// the few visibilities whose w-kernel reaches it, so its inverse FFT is a
+// sum of separable outer products: for a visibility with uv taps at rows
+// a = iu0 + du and columns b = iv0 + dv,
+//   checker(IFFT(layer))[l][m] += kw_j V KU(l) KV(m),
+//   KU(l) = sum_du ku[du] E(iu0 + du, l), E(a, l) = (-1)^(a+l) e^{2 pi i a l / S}
+// (the checkerboards on both sides of the FFT folded into E). Following
+// the recurrence wimg = wimg / D + layer to the end of the tower and the
+// final wimg * D^(last + w_support/2 - 1), a visibility gridded at w-layer
+// P with w-tap j ends up multiplied by D^(P + j - w_support/2), whatever
+// the tower's range. So one workgroup per (sub-grid, 32 x 32
+// pixel tile) keeps the sub-grid image in f64 registers for the whole
+// tower and, per w-layer L, adds the complex rank-n product
+//   M_L = sum_{n : P_n <= L < P_n + w_support} (kw V KU)_n (x) KV_n
+// on the matrix core (4 x v_mfma_f32_16x16x4_f32 per 4 visibilities) after
+// acc = acc / D (as a multiply by the precomputed 1 / D): the stack, its
+// per-layer FFTs and their HBM traffic disappear. Visibilities are staged
+// in an LDS ring (their tap sums over the tile's 32 rows and 32 columns,
+// in f32 like the reference's complex-float layers); the per-layer window
+// comes from an LDS table of layer starts.
+constexpr int kDftCap = 32;      // staged visibilities (ring)
+constexpr int kDftTile = 32;     // tile edge (pixels)
+constexpr int kDftLayers = 512;  // max w-layers of a sub-grid's tower
+constexpr int kDftMaxS = 1024;
+
+struct DftParams
+{
+    TowerParams tp;                 // group's tower parameters
+    const int4* vrec;               // row, channel, layer (rel. P0), gslot
+    const int* seg_start;           // [gslot] first visibility
+    const int* seg_end;             // [gslot] end
+    int64_t gslot_base;             // group * t_cap
+    int64_t P0;
+    Cx<float>* out;                 // [slots][S][S] (stack layer 0)
+    const Cx<double>* wp;           // D
+    const Cx<double>* wp_inv;       // 1 / D
+    const double* uv_kernel;
+    const double* w_kernel;
+};
+
+template<typename U>
+__global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
+        const U* __restrict__ uvws, const Cx<float>* __restrict__ vis)
+{
+#pragma clang fp contract(off)
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    __shared__ float2 s_tw[kDftMaxS];               // e^{2 pi i k / S}
+    __shared__ int s_start[kDftLayers + 1];
+    __shared__ float2 s_aku[kDftCap][kDftTile];     // V KU(l), tile rows
+    __shared__ float2 s_kv[kDftCap][kDftTile];      // KV(m), tile columns
+    __shared__ float s_kw[kDftCap][16];
+    __shared__ int s_tap[kDftCap][4];               // iu0, iv0, u/v offsets
+    __shared__ int s_P[kDftCap];
+
+    const TowerParams& tp = d.tp;
+    const int S = tp.S, ws = tp.w_support, W = tp.support;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int tiles = S / kDftTile;
+    const int L0 = (blockIdx.x / tiles) * kDftTile;
+    const int M0 = (blockIdx.x % tiles) * kDftTile;
+    const int slot = blockIdx.y;
+    const int64_t gs = d.gslot_base + slot;
+    const int s0 = d.seg_start[gs], s1 = d.seg_end[gs];
+    const int n = s1 - s0;
+    // This lane's pixels: block (wave >> 1, wave & 1) of the tile, MFMA
+    // C layout: rows 4 (lane >> 4) + r, column lane & 15.
+    const int bl = (wave >> 1) * 16, bm = (wave & 1) * 16;
+    const int i = lane & 15, kq = lane >> 4;
+    const int pm = M0 + bm + i;
+    Cx<double> acc[4], dinv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        acc[r] = cx<double>(0.0, 0.0);
+        dinv[r] = d.wp_inv[(int64_t)(L0 + bl + 4 * kq + r) * S + pm];
+    }
+    Cx<float>* out = d.out + (int64_t)slot * S * S;
+    if (n <= 0)
+    {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            out[(int64_t)(L0 + bl + 4 * kq + r) * S + pm] = cx<float>(0, 0);
+        return;
+    }
+    for (int k = t; k < S; k += 256)
+    {
+        double sn, cs;
+        sincospi(2.0 * k / S, &sn, &cs);
+        s_tw[k] = make_float2((float)cs, (float)sn);
+    }
+    // Layer starts: s_start[k] = first visibility with P >= P_first + k.
+    // w-layers in the tower's numbering (TowerParams::w_plane).
+    const int shift = (int)(d.P0 - tp.off_w);
+    const int P_first = d.vrec[s0].z + shift, P_last = d.vrec[s1 - 1].z + shift;
+    const int npl = P_last - P_first + 1;
+    if (t == 0)
+    {
+        s_start[0] = 0;
+        s_start[npl] = n;
+    }
+    for (int v = t + 1; v < n; v += 256)
+    {
+        const int pa = d.vrec[s0 + v - 1].z + shift - P_first;
+        const int pb = d.vrec[s0 + v].z + shift - P_first;
+        for (int k = pa + 1; k <= pb; ++k) s_start[k] = v;
+    }
+    const int task = tp.task[slot];
+    const int off_u = (int)((tp.min_iu + task / tp.nv) * tp.eff);
+    const int off_v = (int)((tp.min_iv + task % tp.nv) * tp.eff);
+    int st_lo = 0, st_hi = 0;     // staged range (uniform)
+    __syncthreads();
+
+    const int L_first = P_first, L_last = P_last + ws - 1;
+    for (int L = L_first; L <= L_last; ++L)
+    {
+        const int lo = s_start[max(0, min(npl, L - ws + 1 - P_first))];
+        const int hi = s_start[max(0, min(npl, L + 1 - P_first))];
+        f32x4 c_re = {0.0f, 0.0f, 0.0f, 0.0f};
+        f32x4 c_im = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int a = lo; a < hi; a += kDftCap)
+        {
+            const int b = min(hi, a + kDftCap);
+            if (!(a >= st_lo && b <= st_hi))
+            {
+                // Stage [x, b): keep what is already there when possible.
+                int x = a;
+                if (a >= st_lo && a <= st_hi)
+                {
+                    x = st_hi;
+                    st_lo = max(st_lo, b - kDftCap);
+                }
+                else
+                {
+                    st_lo = a;
+                }
+                st_hi = b;
+                const int cnt = b - x;
+                __syncthreads();   // ring slots free
+                if (t < cnt)
+                {
+                    const int v = x + t, rs = v % kDftCap;
+                    const int4 rec = d.vrec[s0 + v];
+                    TowerParams q = tp;
+                    q.w_plane = (int)(rec.z + d.P0 - tp.off_w);
+                    const Taps2 tt = item_taps(q, uvws, rec.x, rec.y, off_u,
+                            off_v);
+                    s_tap[rs][0] = tt.valid ? tt.iu0 : -1;
+                    s_tap[rs][1] = tt.iv0;
+                    s_tap[rs][2] = tt.u_off;
+                    s_tap[rs][3] = tt.v_off;
+                    s_P[rs] = q.w_plane;
+                    for (int j = 0; j < ws; ++j)
+                        s_kw[rs][j] = tt.valid ?
+                                (float)d.w_kernel[tt.w_off + j] : 0.0f;
+                }
+                __syncthreads();
+                for (int o = t; o < cnt * 2 * kDftTile; o += 256)
+                {
+                    const int v = x + o / (2 * kDftTile);
+                    const int rs = v % kDftCap, q = o % (2 * kDftTile);
+                    const int iu0 = s_tap[rs][0];
+                    float2 res = make_float2(0.0f, 0.0f);
+                    if (iu0 >= 0)
+                    {
+                        const bool row = q < kDftTile;
+                        const int a0 = row ? iu0 : s_tap[rs][1];
+                        const int koff = row ? s_tap[rs][2] : s_tap[rs][3];
+                        const int l = row ? L0 + q : M0 + q - kDftTile;
+                        float sr = 0.0f, si = 0.0f;
+                        for (int du = 0; du < W; ++du)
+                        {
+                            const int aa = a0 + du;
+                            const float k = (float)d.uv_kernel[koff + du];
+                            const float2 e = s_tw[(aa * l) % S];
+                            const float kk = ((aa + l) & 1) ? -k : k;
+                            sr += kk * e.x;
+                            si += kk * e.y;
+                        }
+                        if (row)
+                        {
+                            const int4 rec = d.vrec[s0 + v];
+                            const Cx<float> vv = vis[(int64_t)rec.x *
+                                    tp.num_chan + rec.y];
+                            res = make_float2(vv.re * sr - vv.im * si,
+                                    vv.re * si + vv.im * sr);
+                        }
+                        else
+                        {
+                            res = make_float2(sr, si);
+                        }
+                    }
+                    if (q < kDftTile) s_aku[rs][q] = res;
+                    else s_kv[rs][q - kDftTile] = res;
+                }
+                __syncthreads();
+            }
+            // Complex rank-(b - a) update, four visibilities per step.
+            for (int c4 = a; c4 < b; c4 += 4)
+            {
+                const int v = c4 + kq;
+                const bool ok = v < b;
+                const int rs = (ok ? v : a) % kDftCap;
+                float2 av = s_aku[rs][bl + i];
+                const float2 bv = ok ? s_kv[rs][bm + i] :
+                        make_float2(0.0f, 0.0f);
+                const float kw = ok ? s_kw[rs][L - s_P[rs]] : 0.0f;
+                av.x *= kw;
+                av.y *= kw;
+                c_re = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, c_re,
+                        0, 0, 0);
+                c_re = __builtin_amdgcn_mfma_f32_16x16x4f32(-av.y, bv.y, c_re,
+                        0, 0, 0);
+                c_im = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.y, c_im,
+                        0, 0, 0);
+                c_im = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.x, c_im,
+                        0, 0, 0);
+            }
+        }
+        // wimg = wimg / D + layer.
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            Cx<double> z = cmul(acc[r], dinv[r]);
+            z.re += (double)c_re[r];
+            z.im += (double)c_im[r];
+            acc[r] = z;
+        }
+    }
+    // End of tower: wimg * D^(L_last - w_support / 2) (.cpp:1102-1113),
+    // with the checkerboard of the forward FFT that follows.
+    const int e_final = L_last - ws / 2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+    {
+        const int pl = L0 + bl + 4 * kq + r;
+        const int64_t e = (int64_t)pl * S + pm;
+        Cx<double> z = acc[r];
+        if (e_final != 0) z = cmul(z, cpow_int(d.wp[e], e_final));
+        float re = (float)z.re, im = (float)z.im;
+        if ((pl + pm) & 1)
+        {
+            re = -re;
+            im = -im;
+        }
+        out[e] = cx<float>(re, im);
+    }
+}
+
+__global__ void k_pattern_inv(const Cx<double>* __restrict__ wp,
+        Cx<double>* __restrict__ inv, int64_t n)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < n) inv[i] = cdiv(cx<double>(1.0, 0.0), wp[i]);
+}
+
+// Expand sorted visibility runs (row, c0, c1, slot) into one record per
+// channel: (row, channel, w-layer relative to P0, group slot id).
+__global__ void k_expand_runs(const int4* __restrict__ items,
+        const uint64_t* __restrict__ keys, const int64_t* __restrict__ off,
+        int64_t n_items, int64_t NP, int4* __restrict__ vrec)
+{
+    const int64_t it = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (it >= n_items) return;
+    const int4 r = items[it];
+    const uint64_t key = keys[it];
+    const int p_rel = (int)(key % (uint64_t)NP);
+    const int gslot = (int)(key / (uint64_t)NP);
+    int64_t o = off[it];
+    for (int c = r.y; c < r.z; ++c) vrec[o++] = make_int4(r.x, c, p_rel, gslot);
+}
+
+__global__ void k_run_channels(const int4* __restrict__ items, int64_t n,
+        int64_t* __restrict__ cnt)
+{
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < n) cnt[i] = items[i].z - items[i].y;
+}
+
+__global__ void k_segments(const int4* __restrict__ vrec, int64_t n,
+        int* __restrict__ seg_start, int* __restrict__ seg_end)
+{
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const int gs = vrec[v].w;
+    if (v == 0 || vrec[v - 1].w != gs) seg_start[gs] = (int)v;
+    if (v == n - 1 || vrec[v + 1].w != gs) seg_end[gs] = (int)(v + 1);
+}
+
+// Flags visibilities whose uv taps leave the sub-grid: the reference wraps
+// them through its flat [w_support][S][S] stack indexing, which only the
+// layer-by-layer path reproduces.
+template<typename U>
+__global__ void k_dft_check(const int4* __restrict__ vrec, int64_t n,
+        const U* __restrict__ uvws, TowerParams base,
+        const int* __restrict__ tasks, const int* __restrict__ g_offw,
+        const int* __restrict__ g_tbase, int64_t t_cap, int64_t P0,
+        int* __restrict__ flag)
+{
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    const int4 rec = vrec[v];
+    const int group = (int)(rec.w / t_cap), slot = (int)(rec.w % t_cap);
+    TowerParams q = base;
+    q.off_w = g_offw[group];
+    q.w_plane = (int)(rec.z + P0 - q.off_w);
+    const int task = tasks[g_tbase[group] + slot];
+    const int off_u = (int)((q.min_iu + task / q.nv) * q.eff);
+    const int off_v = (int)((q.min_iv + task % q.nv) * q.eff);
+    const Taps2 tt = item_taps(q, uvws, rec.x, rec.y, off_u, off_v);
+    if (tt.valid && (tt.iu0 < 0 || tt.iu0 + q.support > q.S ||
+            tt.iv0 < 0 || tt.iv0 + q.support > q.S))
+        atomicOr(flag, 1);
+}
+
+// ---------------------------------------------------------------------------
 // Host side.
 
 unsigned blocks_of(int64_t n, int t = 256)
@@ -729,7 +1052,8 @@ enum BufId
 {
     kRowCount, kRowOffset, kOccupied, kSlotMap, kKeys, kKeysAlt, kIdx,
     kIdxAlt, kItemsRaw, kItems, kHist, kTemp, kTasks, kSlotOf, kBounds,
-    kStack, kWimg, kGrid, kNumBuf
+    kStack, kWimg, kGrid, kVrec, kSeg, kRunCnt, kRunOff, kWpInv, kFlag,
+    kGroupInfo, kNumBuf
 };
 
 std::mutex g_mutex;                  // one driver call at a time
@@ -794,6 +1118,7 @@ struct Binned
     std::vector<int> tasks;          // concatenated slot -> task ids
     std::vector<int64_t> offsets;    // [groups][NP + 1] item offsets
     int4* items = nullptr;           // sorted
+    const uint64_t* keys = nullptr;  // sorted keys
     int* d_tasks = nullptr;
     int64_t n_items = 0;
     int64_t t_cap = 0;
@@ -966,6 +1291,7 @@ bool bin_visibilities(const U* d_uvw, Geo& g, size_t budget_bytes,
             kb, vb, (int)n_items, 0, end_bit), status);
     k_gather_items<<<blocks_of(n_items), 256>>>(vb.Current(), d_raw, d_items,
             n_items);
+    out->keys = kb.Current();
     SDP_HIP_CHECK_LAUNCH(status);
     // Item offsets per (group, w-layer).
     std::vector<unsigned int> hist(ng * g.NP);
@@ -1023,11 +1349,106 @@ TowerParams tower_params(const sdp_GridderWtowerUVW* k, const Geo& g,
     return p;
 }
 
+// Fused tower path (k_tower_dft) for complex-float gridding unless
+// SDP_WT_FUSED=0 selects the layer-by-layer path.
+bool dft_enabled()
+{
+    static const bool on = [] {
+        const char* e = std::getenv("SDP_WT_FUSED");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+struct DftData
+{
+    int4* vrec = nullptr;
+    int* seg_start = nullptr;
+    int* seg_end = nullptr;
+    Cx<double>* wp_inv = nullptr;
+};
+
+// Channel records in (group, slot, layer) order, per-slot segments, 1 / D;
+// false (fall back to the layer-by-layer path) if a tower is deeper than
+// kDftLayers or a visibility's taps leave its sub-grid.
+template<typename U>
+bool prepare_dft(const sdp_GridderWtowerUVW* k, const U* d_uvw,
+        const Binned& b, DftData* dd, sdp_Error* status)
+{
+    Workspace& ws = workspace();
+    const Geo& g = b.g;
+    const int64_t ng = (int64_t)b.groups.size();
+    for (const Group& gr : b.groups)
+        if (gr.first_p >= 0 && gr.last_p - gr.first_p + 1 > kDftLayers)
+            return false;
+    const int64_t n = b.n_items;
+    int64_t* d_cnt = (int64_t*)ws.get(kRunCnt, (n + 1) * sizeof(int64_t),
+            status);
+    int64_t* d_off = (int64_t*)ws.get(kRunOff, (n + 1) * sizeof(int64_t),
+            status);
+    if (*status) return false;
+    k_run_channels<<<blocks_of(n), 256>>>(b.items, n, d_cnt);
+    SDP_HIP_CHECK(hipMemsetAsync(d_cnt + n, 0, sizeof(int64_t), 0), status);
+    size_t temp_bytes = 0;
+    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, temp_bytes,
+            d_cnt, d_off, (int)(n + 1)), status);
+    void* d_temp = ws.get(kTemp, temp_bytes, status);
+    if (*status) return false;
+    SDP_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(d_temp, temp_bytes,
+            d_cnt, d_off, (int)(n + 1)), status);
+    int64_t n_vis = 0;
+    SDP_HIP_CHECK(hipMemcpy(&n_vis, d_off + n, sizeof(int64_t),
+            hipMemcpyDeviceToHost), status);
+    if (*status || n_vis > 0x7FFFFFFF) return false;
+    dd->vrec = (int4*)ws.get(kVrec, std::max<int64_t>(n_vis, 1) *
+            sizeof(int4), status);
+    const int64_t nseg = ng * b.t_cap;
+    dd->seg_start = (int*)ws.get(kSeg, 2 * nseg * sizeof(int), status);
+    dd->wp_inv = (Cx<double>*)ws.get(kWpInv,
+            (size_t)g.S * g.S * sizeof(Cx<double>), status);
+    int* d_flag = (int*)ws.get(kFlag, sizeof(int), status);
+    int* d_ginfo = (int*)ws.get(kGroupInfo, 2 * ng * sizeof(int), status);
+    if (*status) return false;
+    dd->seg_end = dd->seg_start + nseg;
+    k_expand_runs<<<blocks_of(n), 256>>>(b.items, b.keys, d_off, n, g.NP,
+            dd->vrec);
+    SDP_HIP_CHECK(hipMemsetAsync(dd->seg_start, 0, 2 * nseg * sizeof(int),
+            0), status);
+    if (n_vis > 0)
+        k_segments<<<blocks_of(n_vis), 256>>>(dd->vrec, n_vis,
+                dd->seg_start, dd->seg_end);
+    k_pattern_inv<<<blocks_of((int64_t)g.S * g.S), 256>>>(
+            (const Cx<double>*)k->d_w_pattern, dd->wp_inv,
+            (int64_t)g.S * g.S);
+    std::vector<int> ginfo(2 * ng);
+    for (int64_t gi = 0; gi < ng; ++gi)
+    {
+        ginfo[gi] = (int)(b.groups[gi].iw * g.H);
+        ginfo[ng + gi] = (int)b.groups[gi].task_base;
+    }
+    SDP_HIP_CHECK(hipMemcpy(d_ginfo, ginfo.data(), ginfo.size() * sizeof(int),
+            hipMemcpyHostToDevice), status);
+    SDP_HIP_CHECK(hipMemsetAsync(d_flag, 0, sizeof(int), 0), status);
+    if (n_vis > 0)
+    {
+        const TowerParams base = tower_params(k, g, b.groups[0], b);
+        k_dft_check<U><<<blocks_of(n_vis), 256>>>(dd->vrec, n_vis, d_uvw,
+                base, b.d_tasks, d_ginfo, d_ginfo + ng, b.t_cap, g.P0,
+                d_flag);
+    }
+    SDP_HIP_CHECK_LAUNCH(status);
+    int flag = 0;
+    SDP_HIP_CHECK(hipMemcpy(&flag, d_flag, sizeof(int),
+            hipMemcpyDeviceToHost), status);
+    return !*status && flag == 0;
+}
+
 struct Timing
 {
     double bin = 0, towers = 0, image = 0;
     int64_t layers = 0;
 };
+
 
 // Grid all visibilities of the selected w-stack planes.
 template<typename T, typename U>
@@ -1045,9 +1466,19 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
     (void)hipMemGetInfo(&free_b, &total_b);
     const size_t budget = std::max<size_t>(per_slot * 64, free_b / 3);
     Binned b;
-    const bool any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b,
-            status);
+    g.fused = (sizeof(T) == 4 && dft_enabled() && g.S % kDftTile == 0 &&
+            g.S <= kDftMaxS && g.w_support <= 16) ? 1 : 0;
+    bool any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b, status);
     if (*status) return;
+    DftData dd;
+    if (b.g.fused && any && !b.groups.empty() && b.n_items > 0 &&
+            !prepare_dft<U>(k, d_uvw, b, &dd, status))
+    {
+        if (*status) return;
+        g.fused = 0;    // layer-by-layer path: re-bin in (layer, slot) order
+        any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b, status);
+        if (*status) return;
+    }
     if (verbosity > 0)
     {
         (void)hipDeviceSynchronize();
@@ -1060,7 +1491,12 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
     Cx<double>* d_wimg = (Cx<double>*)ws.get(kWimg,
             b.t_cap * layer * sizeof(Cx<double>), status);
     Cx<T>* d_grid = (Cx<T>*)ws.get(kGrid, G * G * sizeof(Cx<T>), status);
-    int* d_slot_of = (int*)ws.get(kSlotOf, g.ntask * sizeof(int), status);
+    // Task -> slot maps of all groups, uploaded once: a per-group
+    // hipMemcpyAsync from one reused pageable host vector raced with its
+    // refill for the next group while earlier kernels were still queued.
+    const int64_t ngr = (int64_t)b.groups.size();
+    int* d_slot_of = (int*)ws.get(kSlotOf, ngr * g.ntask * sizeof(int),
+            status);
     sdp_fft::Plan2D* big = cached_plan((int)G, sizeof(T) == 8, 1, G * G,
             status);
     if (*status) return;
@@ -1068,7 +1504,16 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
     const int ws_n = g.w_support;
     const T factor = (T)((double)k->image_size / g.S *
             ((double)k->image_size / g.S));
-    std::vector<int> slot_of(g.ntask);
+    if (!*status)
+    {
+        std::vector<int> slot_of(ngr * g.ntask, -1);
+        for (int64_t gi = 0; gi < ngr; ++gi)
+            for (int64_t sl = 0; sl < b.groups[gi].slots; ++sl)
+                slot_of[gi * g.ntask + b.tasks[b.groups[gi].task_base + sl]] =
+                        (int)sl;
+        SDP_HIP_CHECK(hipMemcpy(d_slot_of, slot_of.data(),
+                slot_of.size() * sizeof(int), hipMemcpyHostToDevice), status);
+    }
     for (size_t gi = 0; gi < b.groups.size() && !*status; ++gi)
     {
         const Group& gr = b.groups[gi];
@@ -1088,57 +1533,84 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
         const int64_t n_el = gr.slots * layer;
         const int64_t ls = p.layer_stride;
         const bool empty = gr.first_p < 0;   // no visibility survived
-        SDP_HIP_CHECK(hipMemsetAsync(d_stack, 0,
-                gr.slots_alloc * layer * ws_n * sizeof(Cx<T>), 0), status);
-        SDP_HIP_CHECK(hipMemsetAsync(d_wimg, 0, n_el * sizeof(Cx<double>),
-                0), status);
-        const int64_t first = empty ? 0 : gr.first_p + g.P0 - p.off_w;
-        const int64_t last = empty ? -1 : gr.last_p + g.P0 - p.off_w;
-        int ring = 0;
-        for (int64_t w_plane = first; w_plane <= last && !*status; ++w_plane)
+        if (g.fused && !empty)
         {
-            if (w_plane != first)
+            if constexpr (sizeof(T) == 4)
             {
-                sdp_fft::exec_2d(sp, d_stack + ring * ls, false, 0, status);
-                k_grid_step<T><<<blocks_of(n_el), 256>>>(d_wimg,
-                        d_stack + ring * ls, wp, layer, g.S, n_el, 1);
-                ring = (ring + 1) % ws_n;
+                DftParams dp;
+                dp.tp = p;
+                dp.vrec = dd.vrec;
+                dp.seg_start = dd.seg_start;
+                dp.seg_end = dd.seg_end;
+                dp.gslot_base = (int64_t)gi * b.t_cap;
+                dp.P0 = g.P0;
+                dp.out = (Cx<float>*)d_stack;
+                dp.wp = wp;
+                dp.wp_inv = dd.wp_inv;
+                dp.uv_kernel = k->d_uv_kernel;
+                dp.w_kernel = k->d_w_kernel;
+                const int tiles = (g.S / kDftTile) * (g.S / kDftTile);
+                k_tower_dft<U><<<dim3(tiles, (unsigned)gr.slots), 256>>>(dp,
+                        d_uvw, (const Cx<float>*)d_vis);
+                SDP_HIP_CHECK_LAUNCH(status);
+                sdp_fft::exec_2d(sp, d_stack, true, 0, status);
             }
-            const int64_t prel = w_plane + p.off_w - g.P0;
-            const int64_t i0 = b.offsets[gi * (g.NP + 1) + prel];
-            const int64_t i1 = b.offsets[gi * (g.NP + 1) + prel + 1];
-            if (i1 > i0)
+            tm.layers += (gr.last_p - gr.first_p + ws_n) * gr.slots;
+        }
+        else if (g.fused)
+        {
+            SDP_HIP_CHECK(hipMemsetAsync(d_stack, 0,
+                    gr.slots_alloc * layer * sizeof(Cx<T>), 0), status);
+        }
+        if (!g.fused)
+        {
+            SDP_HIP_CHECK(hipMemsetAsync(d_stack, 0,
+                    gr.slots_alloc * layer * ws_n * sizeof(Cx<T>), 0), status);
+            SDP_HIP_CHECK(hipMemsetAsync(d_wimg, 0, n_el * sizeof(Cx<double>),
+                    0), status);
+            const int64_t first = empty ? 0 : gr.first_p + g.P0 - p.off_w;
+            const int64_t last = empty ? -1 : gr.last_p + g.P0 - p.off_w;
+            int ring = 0;
+            for (int64_t w_plane = first; w_plane <= last && !*status; ++w_plane)
             {
-                p.w_plane = (int)w_plane;
-                p.ring = ring;
-                k_tower_grid<T, U><<<blocks_of(i1 - i0, kWaves),
-                        64 * kWaves>>>(p, b.items + i0, i1 - i0, d_uvw,
-                        d_stack, k->d_uv_kernel, k->d_w_kernel, d_vis);
+                if (w_plane != first)
+                {
+                    sdp_fft::exec_2d(sp, d_stack + ring * ls, false, 0, status);
+                    k_grid_step<T><<<blocks_of(n_el), 256>>>(d_wimg,
+                            d_stack + ring * ls, wp, layer, g.S, n_el, 1);
+                    ring = (ring + 1) % ws_n;
+                }
+                const int64_t prel = w_plane + p.off_w - g.P0;
+                const int64_t i0 = b.offsets[gi * (g.NP + 1) + prel];
+                const int64_t i1 = b.offsets[gi * (g.NP + 1) + prel + 1];
+                if (i1 > i0)
+                {
+                    p.w_plane = (int)w_plane;
+                    p.ring = ring;
+                    k_tower_grid<T, U><<<blocks_of(i1 - i0, kWaves),
+                            64 * kWaves>>>(p, b.items + i0, i1 - i0, d_uvw,
+                            d_stack, k->d_uv_kernel, k->d_w_kernel, d_vis);
+                }
+                SDP_HIP_CHECK_LAUNCH(status);
             }
-            SDP_HIP_CHECK_LAUNCH(status);
-        }
-        for (int i = 0; i < ws_n && !*status && !empty; ++i)
-        {
-            const int l = (ring + i) % ws_n;
-            sdp_fft::exec_2d(sp, d_stack + l * ls, false, 0, status);
-            k_grid_step<T><<<blocks_of(n_el), 256>>>(d_wimg, d_stack + l * ls,
-                    wp, layer, g.S, n_el, 0);
-        }
-        tm.layers += (last - first + 1) * gr.slots;
-        if (!empty)
-        {
-            k_grid_final<T><<<blocks_of(n_el), 256>>>(d_wimg, d_stack, wp,
-                    layer, g.S, (int)(last + ws_n / 2 - 1), n_el);
-            sdp_fft::exec_2d(sp, d_stack, true, 0, status);
+            for (int i = 0; i < ws_n && !*status && !empty; ++i)
+            {
+                const int l = (ring + i) % ws_n;
+                sdp_fft::exec_2d(sp, d_stack + l * ls, false, 0, status);
+                k_grid_step<T><<<blocks_of(n_el), 256>>>(d_wimg, d_stack + l * ls,
+                        wp, layer, g.S, n_el, 0);
+            }
+            tm.layers += (last - first + 1) * gr.slots;
+            if (!empty)
+            {
+                k_grid_final<T><<<blocks_of(n_el), 256>>>(d_wimg, d_stack, wp,
+                        layer, g.S, (int)(last + ws_n / 2 - 1), n_el);
+                sdp_fft::exec_2d(sp, d_stack, true, 0, status);
+            }
         }
         // Sub-grids into the grid.
-        std::fill(slot_of.begin(), slot_of.end(), -1);
-        for (int64_t s = 0; s < gr.slots; ++s)
-            slot_of[b.tasks[gr.task_base + s]] = (int)s;
-        SDP_HIP_CHECK(hipMemcpyAsync(d_slot_of, slot_of.data(),
-                g.ntask * sizeof(int), hipMemcpyHostToDevice, 0), status);
         k_gather_grid<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(d_grid, G,
-                d_stack, g.S, d_slot_of, g.nu, g.nv, g.min_iu,
+                d_stack, g.S, d_slot_of + gi * g.ntask, g.nu, g.nv, g.min_iu,
                 g.min_iv, g.eff, factor, gr.first_of_plane ? 0 : 1);
         SDP_HIP_CHECK_LAUNCH(status);
         if (verbosity > 0)
@@ -1168,8 +1640,9 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                 "visibility runs, %lld sub-grid w-layers",
                 (long long)g.niw, (long long)g.nu, (long long)g.nv,
                 b.groups.size(), (long long)b.n_items, (long long)tm.layers);
-        SDP_LOG_INFO("| binning %.3f s | towers %.3f s | image side %.3f s",
-                tm.bin, tm.towers, tm.image);
+        SDP_LOG_INFO("| binning %.3f s | towers %.3f s | image side %.3f s"
+                " | %s", tm.bin, tm.towers, tm.image, g.fused ?
+                "fused towers (k_tower_dft)" : "layer-by-layer towers");
     }
 }
 
