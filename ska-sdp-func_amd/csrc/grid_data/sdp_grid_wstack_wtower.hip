@@ -730,6 +730,7 @@ constexpr int kDftCap = 32;      // staged visibilities (ring)
 constexpr int kDftTile = 32;     // tile edge (pixels)
 constexpr int kDftLayers = 512;  // max w-layers of a sub-grid's tower
 constexpr int kDftMaxS = 1024;
+constexpr int kDftBlock = 8;     // w-layers per f32 recurrence block
 
 struct DftParams
 {
@@ -744,6 +745,7 @@ struct DftParams
     const Cx<double>* wp_inv;       // 1 / D
     const double* uv_kernel;
     const double* w_kernel;
+    const float2* tw;               // e^{2 pi i k / S}, k < S
 };
 
 template<typename U>
@@ -756,9 +758,13 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
     __shared__ int s_start[kDftLayers + 1];
     __shared__ float2 s_aku[kDftCap][kDftTile];     // V KU(l), tile rows
     __shared__ float2 s_kv[kDftCap][kDftTile];      // KV(m), tile columns
+    // w taps keyed by absolute w-layer: s_kw[rs][(P + j) % 16] = kw_j,
+    // so the rank update reads kw at layer L without first reading P.
     __shared__ float s_kw[kDftCap][16];
-    __shared__ int s_tap[kDftCap][4];               // iu0, iv0, u/v offsets
+    __shared__ int s_tap[kDftCap][5];   // iu0 (-1: invalid), iv0, u/v/w offsets
     __shared__ int s_P[kDftCap];
+    __shared__ float s_kuv[kDftCap][32];            // u taps, then v taps
+    __shared__ float2 s_V[kDftCap];
 
     const TowerParams& tp = d.tp;
     const int S = tp.S, ws = tp.w_support, W = tp.support;
@@ -775,12 +781,22 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
     const int bl = (wave >> 1) * 16, bm = (wave & 1) * 16;
     const int i = lane & 15, kq = lane >> 4;
     const int pm = M0 + bm + i;
-    Cx<double> acc[4], dinv[4];
+    // The recurrence wimg = wimg / D + M_L runs in f32 within blocks of
+    // kDftBlock layers (acc32, 1 / D rounded to f32) and in f64 across
+    // blocks (acc64 = acc64 / D^kDftBlock + acc32): the reference keeps
+    // wimg in complex double; the block partial sums carry the f32
+    // rounding of kDftBlock steps, like its complex-float layers.
+    Cx<double> acc[4], dinv_k[4];
+    float2 acc32[4], dinv32[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
+        const int64_t e = (int64_t)(L0 + bl + 4 * kq + r) * S + pm;
         acc[r] = cx<double>(0.0, 0.0);
-        dinv[r] = d.wp_inv[(int64_t)(L0 + bl + 4 * kq + r) * S + pm];
+        const Cx<double> di = d.wp_inv[e];
+        dinv32[r] = make_float2((float)di.re, (float)di.im);
+        dinv_k[r] = cpow_int(di, kDftBlock);
+        acc32[r] = make_float2(0.0f, 0.0f);
     }
     Cx<float>* out = d.out + (int64_t)slot * S * S;
     if (n <= 0)
@@ -790,12 +806,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
             out[(int64_t)(L0 + bl + 4 * kq + r) * S + pm] = cx<float>(0, 0);
         return;
     }
-    for (int k = t; k < S; k += 256)
-    {
-        double sn, cs;
-        sincospi(2.0 * k / S, &sn, &cs);
-        s_tw[k] = make_float2((float)cs, (float)sn);
-    }
+    for (int k = t; k < S; k += 256) s_tw[k] = d.tw[k];
     // Layer starts: s_start[k] = first visibility with P >= P_first + k.
     // w-layers in the tower's numbering (TowerParams::w_plane).
     const int shift = (int)(d.P0 - tp.off_w);
@@ -819,6 +830,9 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
     __syncthreads();
 
     const int L_first = P_first, L_last = P_last + ws - 1;
+    // Blocks end at L_last: the first block takes the remainder.
+    const int n_layers = L_last - L_first + 1;
+    const int blk_off = (kDftBlock - n_layers % kDftBlock) % kDftBlock;
     for (int L = L_first; L <= L_last; ++L)
     {
         const int lo = s_start[max(0, min(npl, L - ws + 1 - P_first))];
@@ -830,19 +844,15 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
             const int b = min(hi, a + kDftCap);
             if (!(a >= st_lo && b <= st_hi))
             {
-                // Stage [x, b): keep what is already there when possible.
-                int x = a;
-                if (a >= st_lo && a <= st_hi)
-                {
-                    x = st_hi;
-                    st_lo = max(st_lo, b - kDftCap);
-                }
-                else
-                {
-                    st_lo = a;
-                }
-                st_hi = b;
-                const int cnt = b - x;
+                // Stage ahead: fill the ring with [a, a + kDftCap), keeping
+                // what is already there (windows only move forward, so a
+                // staging pass serves the next few w-layers; each pass
+                // costs several dependent global round trips).
+                const int e = min(n, a + kDftCap);
+                const int x = (a >= st_lo && a <= st_hi) ? st_hi : a;
+                st_lo = a;
+                st_hi = e;
+                const int cnt = e - x;
                 __syncthreads();   // ring slots free
                 if (t < cnt)
                 {
@@ -856,10 +866,32 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                     s_tap[rs][1] = tt.iv0;
                     s_tap[rs][2] = tt.u_off;
                     s_tap[rs][3] = tt.v_off;
+                    s_tap[rs][4] = tt.w_off;
                     s_P[rs] = q.w_plane;
-                    for (int j = 0; j < ws; ++j)
-                        s_kw[rs][j] = tt.valid ?
-                                (float)d.w_kernel[tt.w_off + j] : 0.0f;
+                    const Cx<float> vv = vis[(int64_t)rec.x * tp.num_chan +
+                            rec.y];
+                    s_V[rs] = make_float2(vv.re, vv.im);
+                }
+                __syncthreads();
+                // Kernel rows of the staged visibilities: 2 W uv taps and
+                // w_support w taps each, one load per thread.
+                const int per = 2 * W + ws;
+                for (int o = t; o < cnt * per; o += 256)
+                {
+                    const int v = x + o / per, j = o % per;
+                    const int rs = v % kDftCap;
+                    const bool valid = s_tap[rs][0] >= 0;
+                    if (j < 2 * W)
+                    {
+                        const int koff = s_tap[rs][j < W ? 2 : 3] + j % W;
+                        s_kuv[rs][j] = valid ? (float)d.uv_kernel[koff] : 0.0f;
+                    }
+                    else
+                    {
+                        s_kw[rs][(s_P[rs] + j - 2 * W) & 15] = valid ?
+                                (float)d.w_kernel[s_tap[rs][4] + j - 2 * W] :
+                                0.0f;
+                    }
                 }
                 __syncthreads();
                 for (int o = t; o < cnt * 2 * kDftTile; o += 256)
@@ -872,25 +904,29 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                     {
                         const bool row = q < kDftTile;
                         const int a0 = row ? iu0 : s_tap[rs][1];
-                        const int koff = row ? s_tap[rs][2] : s_tap[rs][3];
+                        const float* kt = s_kuv[rs] + (row ? 0 : W);
                         const int l = row ? L0 + q : M0 + q - kDftTile;
+                        // e^{2 pi i a l / S} for a = a0, a0 + 1, ...: the
+                        // table index advances by l (mod S) per tap and the
+                        // checkerboard sign (-1)^(a + l) alternates.
+                        int idx = (int)(((int64_t)a0 * l) % S);
+                        bool neg = (a0 + l) & 1;
                         float sr = 0.0f, si = 0.0f;
                         for (int du = 0; du < W; ++du)
                         {
-                            const int aa = a0 + du;
-                            const float k = (float)d.uv_kernel[koff + du];
-                            const float2 e = s_tw[(aa * l) % S];
-                            const float kk = ((aa + l) & 1) ? -k : k;
+                            const float2 e = s_tw[idx];
+                            const float kk = neg ? -kt[du] : kt[du];
                             sr += kk * e.x;
                             si += kk * e.y;
+                            idx += l;
+                            if (idx >= S) idx -= S;
+                            neg = !neg;
                         }
                         if (row)
                         {
-                            const int4 rec = d.vrec[s0 + v];
-                            const Cx<float> vv = vis[(int64_t)rec.x *
-                                    tp.num_chan + rec.y];
-                            res = make_float2(vv.re * sr - vv.im * si,
-                                    vv.re * si + vv.im * sr);
+                            const float2 vv = s_V[rs];
+                            res = make_float2(vv.x * sr - vv.y * si,
+                                    vv.x * si + vv.y * sr);
                         }
                         else
                         {
@@ -908,30 +944,39 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                 const int v = c4 + kq;
                 const bool ok = v < b;
                 const int rs = (ok ? v : a) % kDftCap;
-                float2 av = s_aku[rs][bl + i];
-                const float2 bv = ok ? s_kv[rs][bm + i] :
-                        make_float2(0.0f, 0.0f);
-                const float kw = ok ? s_kw[rs][L - s_P[rs]] : 0.0f;
-                av.x *= kw;
-                av.y *= kw;
-                c_re = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, c_re,
+                const float2 av = s_aku[rs][bl + i];
+                const float2 bv = s_kv[rs][bm + i];
+                const float kw = ok ? s_kw[rs][L & 15] : 0.0f;
+                const float ar = av.x * kw, ai = av.y * kw;
+                c_re = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.x, c_re,
                         0, 0, 0);
-                c_re = __builtin_amdgcn_mfma_f32_16x16x4f32(-av.y, bv.y, c_re,
+                c_re = __builtin_amdgcn_mfma_f32_16x16x4f32(-ai, bv.y, c_re,
                         0, 0, 0);
-                c_im = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.y, c_im,
+                c_im = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.y, c_im,
                         0, 0, 0);
-                c_im = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.x, c_im,
+                c_im = __builtin_amdgcn_mfma_f32_16x16x4f32(ai, bv.x, c_im,
                         0, 0, 0);
             }
         }
-        // wimg = wimg / D + layer.
+        // wimg = wimg / D + layer (f32 within the block).
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
-            Cx<double> z = cmul(acc[r], dinv[r]);
-            z.re += (double)c_re[r];
-            z.im += (double)c_im[r];
-            acc[r] = z;
+            const float2 a = acc32[r], q = dinv32[r];
+            acc32[r] = make_float2(a.x * q.x - a.y * q.y + c_re[r],
+                    a.x * q.y + a.y * q.x + c_im[r]);
+        }
+        if ((L - L_first + 1 + blk_off) % kDftBlock == 0)
+        {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                Cx<double> z = cmul(acc[r], dinv_k[r]);
+                z.re += (double)acc32[r].x;
+                z.im += (double)acc32[r].y;
+                acc[r] = z;
+                acc32[r] = make_float2(0.0f, 0.0f);
+            }
         }
     }
     // End of tower: wimg * D^(L_last - w_support / 2) (.cpp:1102-1113),
@@ -952,6 +997,15 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
         }
         out[e] = cx<float>(re, im);
     }
+}
+
+__global__ void k_twiddles(float2* __restrict__ tw, int S)
+{
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= S) return;
+    double sn, cs;
+    sincospi(2.0 * k / S, &sn, &cs);
+    tw[k] = make_float2((float)cs, (float)sn);
 }
 
 __global__ void k_pattern_inv(const Cx<double>* __restrict__ wp,
@@ -1020,6 +1074,17 @@ __global__ void k_dft_check(const int4* __restrict__ vrec, int64_t n,
         atomicOr(flag, 1);
 }
 
+// pswf_n table of a plan's facet (a geometric constant: every w-stack
+// plane's correction divides by the same pswf_n(n(l, m))).
+__global__ void k_pn_table(CorrParams cp, double* __restrict__ tab)
+{
+    const int64_t im = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t il = blockIdx.y;
+    const int N = cp.image_size;
+    if (im >= N) return;
+    tab[il * N + im] = pn_value((int)il - N / 2, (int)im - N / 2, cp);
+}
+
 // ---------------------------------------------------------------------------
 // Host side.
 
@@ -1053,7 +1118,7 @@ enum BufId
     kRowCount, kRowOffset, kOccupied, kSlotMap, kKeys, kKeysAlt, kIdx,
     kIdxAlt, kItemsRaw, kItems, kHist, kTemp, kTasks, kSlotOf, kBounds,
     kStack, kWimg, kGrid, kVrec, kSeg, kRunCnt, kRunOff, kWpInv, kFlag,
-    kGroupInfo, kNumBuf
+    kGroupInfo, kTwiddle, kNumBuf
 };
 
 std::mutex g_mutex;                  // one driver call at a time
@@ -1099,6 +1164,31 @@ sdp_GridderWtowerUVW* cached_kernel(int image_size, int S, double theta,
     }
     cache[key] = k;
     return k;
+}
+
+// Correction parameters with the plan's cached pswf_n table (built on
+// first use; plans are cached for the process lifetime by cached_kernel).
+CorrParams corr_params_tab(const sdp_GridderWtowerUVW* k, int w_offset,
+        bool inverse, sdp_Error* status)
+{
+    static std::map<const void*, double*> tabs;
+    CorrParams cp = corr_params(k, w_offset, inverse);
+    auto it = tabs.find(k);
+    if (it == tabs.end())
+    {
+        const int64_t N = k->image_size;
+        double* d = nullptr;
+        if (hipMalloc(&d, N * N * sizeof(double)) != hipSuccess)
+        {
+            (void)hipGetLastError();
+            return cp;    // no room: evaluate per pixel
+        }
+        k_pn_table<<<dim3(blocks_of(N), (unsigned)N), 256>>>(cp, d);
+        SDP_HIP_CHECK_LAUNCH(status);
+        it = tabs.emplace(k, d).first;
+    }
+    cp.pn_tab = it->second;
+    return cp;
 }
 
 // One (w-stack plane, batch of sub-grids) unit of work.
@@ -1366,6 +1456,7 @@ struct DftData
     int* seg_start = nullptr;
     int* seg_end = nullptr;
     Cx<double>* wp_inv = nullptr;
+    float2* tw = nullptr;
 };
 
 // Channel records in (group, slot, layer) order, per-slot segments, 1 / D;
@@ -1407,6 +1498,7 @@ bool prepare_dft(const sdp_GridderWtowerUVW* k, const U* d_uvw,
     dd->wp_inv = (Cx<double>*)ws.get(kWpInv,
             (size_t)g.S * g.S * sizeof(Cx<double>), status);
     int* d_flag = (int*)ws.get(kFlag, sizeof(int), status);
+    dd->tw = (float2*)ws.get(kTwiddle, g.S * sizeof(float2), status);
     int* d_ginfo = (int*)ws.get(kGroupInfo, 2 * ng * sizeof(int), status);
     if (*status) return false;
     dd->seg_end = dd->seg_start + nseg;
@@ -1417,6 +1509,7 @@ bool prepare_dft(const sdp_GridderWtowerUVW* k, const U* d_uvw,
     if (n_vis > 0)
         k_segments<<<blocks_of(n_vis), 256>>>(dd->vrec, n_vis,
                 dd->seg_start, dd->seg_end);
+    k_twiddles<<<blocks_of(g.S), 256>>>(dd->tw, g.S);
     k_pattern_inv<<<blocks_of((int64_t)g.S * g.S), 256>>>(
             (const Cx<double>*)k->d_w_pattern, dd->wp_inv,
             (int64_t)g.S * g.S);
@@ -1467,7 +1560,7 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
     const size_t budget = std::max<size_t>(per_slot * 64, free_b / 3);
     Binned b;
     g.fused = (sizeof(T) == 4 && dft_enabled() && g.S % kDftTile == 0 &&
-            g.S <= kDftMaxS && g.w_support <= 16) ? 1 : 0;
+            g.S <= kDftMaxS && g.w_support <= 16 && g.support <= 16) ? 1 : 0;
     bool any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b, status);
     if (*status) return;
     DftData dd;
@@ -1549,6 +1642,7 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                 dp.wp_inv = dd.wp_inv;
                 dp.uv_kernel = k->d_uv_kernel;
                 dp.w_kernel = k->d_w_kernel;
+                dp.tw = dd.tw;
                 const int tiles = (g.S / kDftTile) * (g.S / kDftTile);
                 k_tower_dft<U><<<dim3(tiles, (unsigned)gr.slots), 256>>>(dp,
                         d_uvw, (const Cx<float>*)d_vis);
@@ -1622,7 +1716,8 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
         {
             const double ti = now_s();
             sdp_fft::exec_2d(big, d_grid, false, 0, status);
-            const CorrParams cp = corr_params(k, (int)(gr.iw * g.H), true);
+            const CorrParams cp = corr_params_tab(k, (int)(gr.iw * g.H), true,
+                    status);
             k_image_update<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
                     d_grid, G, image, (T)(1.0 / ((double)G * G)), cp);
             SDP_HIP_CHECK_LAUNCH(status);
@@ -1689,7 +1784,8 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
         if (gr.first_of_plane)
         {
             const double ti = now_s();
-            const CorrParams cp = corr_params(k, (int)(gr.iw * g.H), false);
+            const CorrParams cp = corr_params_tab(k, (int)(gr.iw * g.H),
+                    false, status);
             k_image_to_grid<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
                     image, G, d_grid, cp);
             SDP_HIP_CHECK_LAUNCH(status);

@@ -632,6 +632,7 @@ CorrParams corr_params(const sdp_GridderWtowerUVW* plan, int w_offset,
     cp.c_n = plan->w_support * (M_PI / 2);
     cp.w_offset = w_offset;
     cp.inverse = inverse ? 1 : 0;
+    cp.pn_tab = nullptr;
     return cp;
 }
 

@@ -58,7 +58,21 @@ struct CorrParams
     double c_n;
     int w_offset;
     int inverse;              // grid_correct (1) or degrid_correct (0)
+    const double* pn_tab;     // optional [image_size^2] table of pn_value
 };
+
+// pswf_n(|2 w_step n|) of pixel (pl, pm) (1 outside the PSWF's support).
+__device__ __forceinline__ double pn_value(int pl, int pm,
+        const CorrParams& cp)
+{
+#pragma clang fp contract(off)
+    if (!(cp.c_n > 0.0)) return 1.0;
+    const double l = pl * cp.theta / cp.image_size;
+    const double m = pm * cp.theta / cp.image_size;
+    const double n = lm_to_n_dev(l, m, cp.shear_u, cp.shear_v);
+    const double n_x = fabs(n * 2.0 * cp.w_step);
+    return (n_x < 1.0) ? pswf_eval(cp.pswf_n, cp.n_pswf_n, n_x) : 1.0;
+}
 
 CorrParams corr_params(const sdp_GridderWtowerUVW* plan, int w_offset,
         bool inverse);
@@ -80,13 +94,10 @@ __device__ __forceinline__ Cx<double> correct_value(Cx<double> z, int kind,
     const double m = pm * cp.theta / cp.image_size;
     const double p_l = cp.pswf_lm[pl + half];
     const double p_m = cp.pswf_lm[pm + half];
-    double p_n = 1.0;
     const double n = lm_to_n_dev(l, m, cp.shear_u, cp.shear_v);
-    if (cp.c_n > 0.0)
-    {
-        const double n_x = fabs(n * 2.0 * cp.w_step);
-        p_n = (n_x < 1.0) ? pswf_eval(cp.pswf_n, cp.n_pswf_n, n_x) : 1.0;
-    }
+    const double p_n = cp.pn_tab ?
+            cp.pn_tab[(int64_t)(pl + half) * cp.image_size + (pm + half)] :
+            pn_value(pl, pm, cp);
     const double scale = 1.0 / (p_l * p_m * p_n);
     if (kind <= 1)
     {
