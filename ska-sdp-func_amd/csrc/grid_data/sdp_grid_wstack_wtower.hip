@@ -702,6 +702,17 @@ __global__ void k_image_to_grid(AnyView image, int64_t G,
 }
 
 // ---------------------------------------------------------------------------
+// Workgroup barrier that first drains this wave's LDS operations. Without
+// the explicit lgkmcnt(0), a barrier on a loop back-edge of k_tower_idft
+// was reached with an LDS store still in flight and another wave's read
+// after the barrier missed it (about 1 in 2000 visibilities lost one
+// 16 x 16 block's partial).
+__device__ __forceinline__ void lds_sync()
+{
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+    __syncthreads();
+}
+
 // Fused w-tower gridding for complex-float visibilities (k_tower_dft).
 //
 // The reference moves a w_support-deep stack of S x S sub-grids through
@@ -746,6 +757,8 @@ struct DftParams
     const double* uv_kernel;
     const double* w_kernel;
     const float2* tw;               // e^{2 pi i k / S}, k < S
+    const Cx<float>* in;            // degrid: [slots][S][S] sub-grid images
+    float2* part;                   // degrid: [visibility][tile] partials
 };
 
 template<typename U>
@@ -827,7 +840,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
     const int off_u = (int)((tp.min_iu + task / tp.nv) * tp.eff);
     const int off_v = (int)((tp.min_iv + task % tp.nv) * tp.eff);
     int st_lo = 0, st_hi = 0;     // staged range (uniform)
-    __syncthreads();
+    lds_sync();
 
     const int L_first = P_first, L_last = P_last + ws - 1;
     // Blocks end at L_last: the first block takes the remainder.
@@ -853,7 +866,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                 st_lo = a;
                 st_hi = e;
                 const int cnt = e - x;
-                __syncthreads();   // ring slots free
+                lds_sync();   // ring slots free
                 if (t < cnt)
                 {
                     const int v = x + t, rs = v % kDftCap;
@@ -872,7 +885,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                             rec.y];
                     s_V[rs] = make_float2(vv.re, vv.im);
                 }
-                __syncthreads();
+                lds_sync();
                 // Kernel rows of the staged visibilities: 2 W uv taps and
                 // w_support w taps each, one load per thread.
                 const int per = 2 * W + ws;
@@ -893,7 +906,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                                 0.0f;
                     }
                 }
-                __syncthreads();
+                lds_sync();
                 for (int o = t; o < cnt * 2 * kDftTile; o += 256)
                 {
                     const int v = x + o / (2 * kDftTile);
@@ -936,7 +949,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                     if (q < kDftTile) s_aku[rs][q] = res;
                     else s_kv[rs][q - kDftTile] = res;
                 }
-                __syncthreads();
+                lds_sync();
             }
             // Complex rank-(b - a) update, four visibilities per step.
             for (int c4 = a; c4 < b; c4 += 4)
@@ -997,6 +1010,297 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
         }
         out[e] = cx<float>(re, im);
     }
+}
+
+// Fused w-tower degridding for complex-float visibilities (k_tower_idft),
+// the adjoint of k_tower_dft. The reference fills a w_support-deep stack
+// with forward FFTs of wimg / D^k and reads each visibility's taps from it
+// (sdp_gridder_wtower_uvw.cpp:726-909); with X the sub-grid image after
+// the inverse FFT of its cut-out, a visibility gridded at w-layer P reads
+//   vis += sum_j kw_j sum_{l,m} X[l][m] D^-(P + j - w_support/2)[l][m]
+//          conj(KU)(l) conj(KV)(m)
+// (KU, KV as in k_tower_dft). One workgroup per (sub-grid, 32 x 32 pixel
+// tile) keeps Y_L = X D^-(L - w_support/2) in registers (f32 within
+// kDftBlock layers, re-anchored from f64 across blocks) and, per w-layer,
+// forms T = Y_L conj(KV) for 16 visibilities on the matrix core
+// (16 x v_mfma_f32_16x16x4_f32 per 16 x 16 pixel block), contracts T with
+// conj(KU) on the lanes and accumulates kw-weighted partials per
+// visibility in LDS. Partials of a (visibility, tile) pair are added to a
+// scratch row owned by the workgroup; k_idft_reduce sums the rows.
+template<typename U>
+__global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
+        const U* __restrict__ uvws)
+{
+#pragma clang fp contract(off)
+    using f32x4 = __attribute__((ext_vector_type(4))) float;
+    __shared__ float2 s_tw[kDftMaxS];
+    __shared__ int s_start[kDftLayers + 1];
+    __shared__ float2 s_ku[kDftCap][kDftTile];      // conj KU(l), tile rows
+    __shared__ float2 s_kv[kDftCap][kDftTile];      // conj KV(m), tile cols
+    __shared__ float s_kw[kDftCap][16];             // keyed by w-layer % 16
+    __shared__ int s_tap[kDftCap][5];
+    __shared__ int s_P[kDftCap];
+    __shared__ float s_kuv[kDftCap][32];
+    __shared__ float2 s_acc[4][kDftCap];            // per-wave partials
+
+    const TowerParams& tp = d.tp;
+    const int S = tp.S, ws = tp.w_support, W = tp.support;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int tiles = S / kDftTile;
+    const int tile = blockIdx.x;
+    const int L0 = (tile / tiles) * kDftTile;
+    const int M0 = (tile % tiles) * kDftTile;
+    const int slot = blockIdx.y;
+    const int64_t gs = d.gslot_base + slot;
+    const int s0 = d.seg_start[gs], s1 = d.seg_end[gs];
+    const int n = s1 - s0;
+    if (n <= 0) return;
+    const int ntiles = tiles * tiles;
+    const int bl = (wave >> 1) * 16, bm = (wave & 1) * 16;
+    const int i = lane & 15, kq = lane >> 4;
+    const int shift = (int)(d.P0 - tp.off_w);
+    const int P_first = d.vrec[s0].z + shift, P_last = d.vrec[s1 - 1].z + shift;
+    const int npl = P_last - P_first + 1;
+    const int L_first = P_first, L_last = P_last + ws - 1;
+
+    // A-operand pixels of this lane: row bl + i, columns bm + 4 kk + kq.
+    Cx<double> y64[4], dinv_k[4];
+    float2 y32[4], dinv32[4];
+    const Cx<float>* X = d.in + (int64_t)slot * S * S;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+    {
+        const int64_t e = (int64_t)(L0 + bl + i) * S + (M0 + bm + 4 * kk + kq);
+        const Cx<float> x = X[e];
+        y64[kk] = cmul(cx<double>((double)x.re, (double)x.im),
+                cpow_int(d.wp[e], -(L_first - ws / 2)));
+        const Cx<double> di = d.wp_inv[e];
+        dinv32[kk] = make_float2((float)di.re, (float)di.im);
+        dinv_k[kk] = cpow_int(di, kDftBlock);
+        y32[kk] = make_float2((float)y64[kk].re, (float)y64[kk].im);
+    }
+    for (int k = t; k < S; k += 256) s_tw[k] = d.tw[k];
+    for (int k = t; k < 4 * kDftCap; k += 256)
+        s_acc[k / kDftCap][k % kDftCap] = make_float2(0.0f, 0.0f);
+    if (t == 0)
+    {
+        s_start[0] = 0;
+        s_start[npl] = n;
+    }
+    for (int v = t + 1; v < n; v += 256)
+    {
+        const int pa = d.vrec[s0 + v - 1].z + shift - P_first;
+        const int pb = d.vrec[s0 + v].z + shift - P_first;
+        for (int k = pa + 1; k <= pb; ++k) s_start[k] = v;
+    }
+    const int task = tp.task[slot];
+    const int off_u = (int)((tp.min_iu + task / tp.nv) * tp.eff);
+    const int off_v = (int)((tp.min_iv + task % tp.nv) * tp.eff);
+    int st_lo = 0, st_hi = 0;
+    lds_sync();
+
+    // Adds the partials of staged visibilities [f0, f1) to their scratch
+    // rows and clears them (call between barriers). Visibility v is always
+    // flushed by thread v % 256, so a scratch entry's read-modify-writes
+    // stay in one thread's program order.
+    auto flush = [&](int f0, int f1) {
+        for (int v = f0 + ((t - f0) % 256 + 256) % 256; v < f1; v += 256)
+        {
+            const int rs = v % kDftCap;
+            float2 sum = make_float2(0.0f, 0.0f);
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+            {
+                sum.x += s_acc[w][rs].x;
+                sum.y += s_acc[w][rs].y;
+                s_acc[w][rs] = make_float2(0.0f, 0.0f);
+            }
+            float2* dst = d.part + (int64_t)(s0 + v) * ntiles + tile;
+            const float2 old = *dst;
+            *dst = make_float2(old.x + sum.x, old.y + sum.y);
+        }
+    };
+
+    for (int L = L_first; L <= L_last; ++L)
+    {
+        const int lo = s_start[max(0, min(npl, L - ws + 1 - P_first))];
+        const int hi = s_start[max(0, min(npl, L + 1 - P_first))];
+        for (int a = lo; a < hi; a += kDftCap)
+        {
+            const int b = min(hi, a + kDftCap);
+            if (!(a >= st_lo && b <= st_hi))
+            {
+                const int e = min(n, a + kDftCap);
+                const bool keep = a >= st_lo && a <= st_hi;
+                const int x = keep ? st_hi : a;
+                lds_sync();   // all partials of the ring written
+                if (keep) flush(st_lo, a);
+                else flush(st_lo, st_hi);
+                st_lo = a;
+                st_hi = e;
+                const int cnt = e - x;
+                if (t < cnt)
+                {
+                    const int v = x + t, rs = v % kDftCap;
+                    const int4 rec = d.vrec[s0 + v];
+                    TowerParams q = tp;
+                    q.w_plane = (int)(rec.z + d.P0 - tp.off_w);
+                    const Taps2 tt = item_taps(q, uvws, rec.x, rec.y, off_u,
+                            off_v);
+                    s_tap[rs][0] = tt.valid ? tt.iu0 : -1;
+                    s_tap[rs][1] = tt.iv0;
+                    s_tap[rs][2] = tt.u_off;
+                    s_tap[rs][3] = tt.v_off;
+                    s_tap[rs][4] = tt.w_off;
+                    s_P[rs] = q.w_plane;
+                }
+                lds_sync();
+                const int per = 2 * W + ws;
+                for (int o = t; o < cnt * per; o += 256)
+                {
+                    const int v = x + o / per, j = o % per;
+                    const int rs = v % kDftCap;
+                    const bool valid = s_tap[rs][0] >= 0;
+                    if (j < 2 * W)
+                    {
+                        const int koff = s_tap[rs][j < W ? 2 : 3] + j % W;
+                        s_kuv[rs][j] = valid ? (float)d.uv_kernel[koff] : 0.0f;
+                    }
+                    else
+                    {
+                        s_kw[rs][(s_P[rs] + j - 2 * W) & 15] = valid ?
+                                (float)d.w_kernel[s_tap[rs][4] + j - 2 * W] :
+                                0.0f;
+                    }
+                }
+                lds_sync();
+                for (int o = t; o < cnt * 2 * kDftTile; o += 256)
+                {
+                    const int v = x + o / (2 * kDftTile);
+                    const int rs = v % kDftCap, q = o % (2 * kDftTile);
+                    const int iu0 = s_tap[rs][0];
+                    float2 res = make_float2(0.0f, 0.0f);
+                    if (iu0 >= 0)
+                    {
+                        const bool row = q < kDftTile;
+                        const int a0 = row ? iu0 : s_tap[rs][1];
+                        const float* kt = s_kuv[rs] + (row ? 0 : W);
+                        const int l = row ? L0 + q : M0 + q - kDftTile;
+                        int idx = (int)(((int64_t)a0 * l) % S);
+                        bool neg = (a0 + l) & 1;
+                        float sr = 0.0f, si = 0.0f;
+                        for (int du = 0; du < W; ++du)
+                        {
+                            const float2 ew = s_tw[idx];
+                            const float kk = neg ? -kt[du] : kt[du];
+                            sr += kk * ew.x;
+                            si += kk * ew.y;
+                            idx += l;
+                            if (idx >= S) idx -= S;
+                            neg = !neg;
+                        }
+                        res = make_float2(sr, -si);   // conjugate
+                    }
+                    if (q < kDftTile) s_ku[rs][q] = res;
+                    else s_kv[rs][q - kDftTile] = res;
+                }
+                lds_sync();
+            }
+            // 16 visibilities per step: T = Y_L conj(KV) on the matrix core.
+            for (int c16 = a; c16 < b; c16 += 16)
+            {
+                const int v = c16 + i;
+                const bool ok = v < b;
+                const int rs = (ok ? v : a) % kDftCap;
+                f32x4 t_re = {0.0f, 0.0f, 0.0f, 0.0f};
+                f32x4 t_im = {0.0f, 0.0f, 0.0f, 0.0f};
+                float2 bv[4];
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                {
+                    bv[kk] = s_kv[rs][bm + 4 * kk + kq];
+                    if (!ok) bv[kk] = make_float2(0.0f, 0.0f);
+                }
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                {
+                    const float yr = y32[kk].x, yi = y32[kk].y;
+                    t_re = __builtin_amdgcn_mfma_f32_16x16x4f32(yr, bv[kk].x,
+                            t_re, 0, 0, 0);
+                    t_re = __builtin_amdgcn_mfma_f32_16x16x4f32(-yi, bv[kk].y,
+                            t_re, 0, 0, 0);
+                    t_im = __builtin_amdgcn_mfma_f32_16x16x4f32(yr, bv[kk].y,
+                            t_im, 0, 0, 0);
+                    t_im = __builtin_amdgcn_mfma_f32_16x16x4f32(yi, bv[kk].x,
+                            t_im, 0, 0, 0);
+                }
+                // Rows 4 kq + r of T for visibility i: contract with conj KU.
+                float pr = 0.0f, pi = 0.0f;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    const float2 ku = s_ku[rs][bl + 4 * kq + r];
+                    pr += ku.x * t_re[r] - ku.y * t_im[r];
+                    pi += ku.x * t_im[r] + ku.y * t_re[r];
+                }
+                pr += __shfl_xor(pr, 16);
+                pi += __shfl_xor(pi, 16);
+                pr += __shfl_xor(pr, 32);
+                pi += __shfl_xor(pi, 32);
+                if (kq == 0 && ok)
+                {
+                    const float kw = s_kw[rs][L & 15];
+                    float2 acc = s_acc[wave][rs];
+                    acc.x += pr * kw;
+                    acc.y += pi * kw;
+                    s_acc[wave][rs] = acc;
+                }
+            }
+        }
+        // Y_{L+1} = Y_L / D.
+        if ((L + 1 - L_first) % kDftBlock == 0)
+        {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+            {
+                y64[kk] = cmul(y64[kk], dinv_k[kk]);
+                y32[kk] = make_float2((float)y64[kk].re, (float)y64[kk].im);
+            }
+        }
+        else
+        {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+            {
+                const float2 yv = y32[kk], q = dinv32[kk];
+                y32[kk] = make_float2(yv.x * q.x - yv.y * q.y,
+                        yv.x * q.y + yv.y * q.x);
+            }
+        }
+    }
+    lds_sync();
+    flush(st_lo, st_hi);
+}
+
+// vis[row, channel] += sum over the tiles of the scratch row.
+__global__ void k_idft_reduce(const int4* __restrict__ vrec, int64_t n_vis,
+        const float2* __restrict__ part, int ntiles, int64_t num_chan,
+        Cx<float>* __restrict__ vis)
+{
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (v >= n_vis) return;
+    const float2* p = part + v * ntiles;
+    float sr = 0.0f, si = 0.0f;
+    for (int k = 0; k < ntiles; ++k)
+    {
+        const float2 x = p[k];
+        sr += x.x;
+        si += x.y;
+    }
+    const int4 rec = vrec[v];
+    Cx<float>* out = vis + (int64_t)rec.x * num_chan + rec.y;
+    atomicAdd(&out->re, sr);
+    atomicAdd(&out->im, si);
 }
 
 __global__ void k_twiddles(float2* __restrict__ tw, int S)
@@ -1118,7 +1422,7 @@ enum BufId
     kRowCount, kRowOffset, kOccupied, kSlotMap, kKeys, kKeysAlt, kIdx,
     kIdxAlt, kItemsRaw, kItems, kHist, kTemp, kTasks, kSlotOf, kBounds,
     kStack, kWimg, kGrid, kVrec, kSeg, kRunCnt, kRunOff, kWpInv, kFlag,
-    kGroupInfo, kTwiddle, kNumBuf
+    kGroupInfo, kTwiddle, kPart, kNumBuf
 };
 
 std::mutex g_mutex;                  // one driver call at a time
@@ -1457,6 +1761,7 @@ struct DftData
     int* seg_end = nullptr;
     Cx<double>* wp_inv = nullptr;
     float2* tw = nullptr;
+    int64_t n_vis = 0;
 };
 
 // Channel records in (group, slot, layer) order, per-slot segments, 1 / D;
@@ -1502,6 +1807,7 @@ bool prepare_dft(const sdp_GridderWtowerUVW* k, const U* d_uvw,
     int* d_ginfo = (int*)ws.get(kGroupInfo, 2 * ng * sizeof(int), status);
     if (*status) return false;
     dd->seg_end = dd->seg_start + nseg;
+    dd->n_vis = n_vis;
     k_expand_runs<<<blocks_of(n), 256>>>(b.items, b.keys, d_off, n, g.NP,
             dd->vrec);
     SDP_HIP_CHECK(hipMemsetAsync(dd->seg_start, 0, 2 * nseg * sizeof(int),
@@ -1757,9 +2063,33 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
     (void)hipMemGetInfo(&free_b, &total_b);
     const size_t budget = std::max<size_t>(per_slot * 64, free_b / 3);
     Binned b;
-    const bool any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b,
-            status);
+    g.fused = (sizeof(T) == 4 && dft_enabled() && g.S % kDftTile == 0 &&
+            g.S <= kDftMaxS && g.w_support <= 16 && g.support <= 16) ? 1 : 0;
+    bool any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b, status);
     if (*status) return;
+    DftData dd;
+    const int ntiles = (g.S / kDftTile) * (g.S / kDftTile);
+    float2* d_part = nullptr;
+    if (b.g.fused && any && !b.groups.empty() && b.n_items > 0)
+    {
+        bool ok = prepare_dft<U>(k, d_uvw, b, &dd, status);
+        if (*status) return;
+        const size_t part_bytes = (size_t)std::max<int64_t>(dd.n_vis, 1) *
+                ntiles * sizeof(float2);
+        if (ok && part_bytes <= free_b / 3)
+        {
+            d_part = (float2*)ws.get(kPart, part_bytes, status);
+            SDP_HIP_CHECK(hipMemsetAsync(d_part, 0, part_bytes, 0), status);
+            if (*status) return;
+        }
+        else
+        {
+            g.fused = 0;   // layer-by-layer path: re-bin in (layer, slot) order
+            any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b,
+                    status);
+            if (*status) return;
+        }
+    }
     if (verbosity > 0)
     {
         (void)hipDeviceSynchronize();
@@ -1819,6 +2149,38 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
         sdp_fft::exec_2d(sp, d_wimg, false, 0, status);
         const int64_t first = gr.first_p + g.P0 - p.off_w;
         const int64_t last = gr.last_p + g.P0 - p.off_w;
+        if (g.fused)
+        {
+            if constexpr (sizeof(T) == 4)
+            {
+                k_degrid_init<T><<<blocks_of(n_el), 256>>>(d_wimg, wp, layer,
+                        g.S, norm, 0, n_el);
+                DftParams dp = {};
+                dp.tp = p;
+                dp.vrec = dd.vrec;
+                dp.seg_start = dd.seg_start;
+                dp.seg_end = dd.seg_end;
+                dp.gslot_base = (int64_t)gi * b.t_cap;
+                dp.P0 = g.P0;
+                dp.wp = wp;
+                dp.wp_inv = dd.wp_inv;
+                dp.uv_kernel = k->d_uv_kernel;
+                dp.w_kernel = k->d_w_kernel;
+                dp.tw = dd.tw;
+                dp.in = (const Cx<float>*)d_wimg;
+                dp.part = d_part;
+                k_tower_idft<U><<<dim3(ntiles, (unsigned)gr.slots), 256>>>(
+                        dp, d_uvw);
+                SDP_HIP_CHECK_LAUNCH(status);
+            }
+            tm.layers += (last - first + ws_n) * gr.slots;
+            if (verbosity > 0)
+            {
+                (void)hipDeviceSynchronize();
+                tm.towers += now_s() - tg;
+            }
+            continue;
+        }
         k_degrid_init<T><<<blocks_of(n_el), 256>>>(d_wimg, wp, layer, g.S,
                 norm, (int)(first - ws_n / 2), n_el);
         for (int i = 0; i < ws_n && !*status; ++i)
@@ -1859,6 +2221,15 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
             tm.towers += now_s() - tg;
         }
     }
+    if (g.fused && d_part && !*status && dd.n_vis > 0)
+    {
+        if constexpr (sizeof(T) == 4)
+        {
+            k_idft_reduce<<<blocks_of(dd.n_vis), 256>>>(dd.vrec, dd.n_vis,
+                    d_part, ntiles, g.num_chan, (Cx<float>*)d_vis);
+            SDP_HIP_CHECK_LAUNCH(status);
+        }
+    }
     if (verbosity > 0 && !*status)
     {
         SDP_LOG_INFO("w-stacking with w-towers (degridding): %lld w-stack "
@@ -1866,8 +2237,9 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
                 "visibility runs, %lld sub-grid w-layers",
                 (long long)g.niw, (long long)g.nu, (long long)g.nv,
                 b.groups.size(), (long long)b.n_items, (long long)tm.layers);
-        SDP_LOG_INFO("| binning %.3f s | towers %.3f s | image side %.3f s",
-                tm.bin, tm.towers, tm.image);
+        SDP_LOG_INFO("| binning %.3f s | towers %.3f s | image side %.3f s"
+                " | %s", tm.bin, tm.towers, tm.image, g.fused ?
+                "fused towers (k_tower_idft)" : "layer-by-layer towers");
     }
 }
 
