@@ -1,5 +1,6 @@
 """Gridding functions (reference: src/ska_sdp_func/grid_data/__init__.py)."""
 
+from .degrid_uvw_custom import degrid_uvw_custom
 from .gridder_utils import (
     clamp_channels_single,
     clamp_channels_uv,
@@ -27,6 +28,7 @@ __all__ = [
     "GridderUvwEsFft",
     "GridderWtowerUVW",
     "clamp_channels_single",
+    "degrid_uvw_custom",
     "clamp_channels_uv",
     "determine_max_w_tower_height",
     "determine_w_step",
