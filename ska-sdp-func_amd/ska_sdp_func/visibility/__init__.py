@@ -1,9 +1,12 @@
 """Visibility-domain functions (mirror of src/ska_sdp_func/visibility)."""
 
+from .dft import dft_point_v00, dft_point_v01
 from .flagger import flagger_dynamic_threshold
 from .weighting import briggs_weights, get_uv_range, uniform_weights
 
 __all__ = [
+    "dft_point_v00",
+    "dft_point_v01",
     "flagger_dynamic_threshold",
     "briggs_weights",
     "get_uv_range",
