@@ -282,7 +282,8 @@ def main():
     dom = max(avg, key=lambda k: avg[k]) if any(avg.values()) else "tile_kernel"
     achieved = (kern_bytes[dom] / (avg[dom] * 1e-3) / 1e9
                 if avg.get(dom) else None)
-    kernel_names = {"tile_kernel": "k_scatter_mfma (MFMA tile accumulation)",
+    kernel_names = {"tile_kernel": "k_scatter_tab (MFMA tile accumulation, "
+                                   "LDS tap tables)",
                     "fft": ("k_rows_grid + k_cols_a_grid (pruned FFT passes)"
                             if plan.fused_fft else "rocFFT 2-D C2C inverse"),
                     "bucket": "bucketing (count/scan/fill)",

@@ -20,8 +20,9 @@ import sys
 PHASES = {
     "bucket": ("k_bucket_count", "k_scan_columns", "k_scan_bins",
                "k_bucket_fill", "k_zero_shared_tiles"),
-    "tile_kernel": ("k_scatter_mfma", "k_scatter<", "k_scatter(",
-                    "k_gather_mfma", "k_gather<", "k_gather("),
+    "tile_kernel": ("k_scatter_tab", "k_scatter_mfma", "k_scatter<",
+                    "k_scatter(", "k_gather_tab", "k_gather_mfma", "k_gather<",
+                    "k_gather("),
     "image": ("k_screen_corr_2d", "k_screen_accumulate", "k_apply_correction",
               "k_reverse_screen", "k_cols_b_grid"),
     # fused FFT passes (es_fft.hip); rocFFT kernels match "fft" below
