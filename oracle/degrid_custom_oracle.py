@@ -43,6 +43,9 @@ def degrid(grid, uvw, uv_kernel, w_kernel, theta, wstep, f0, df, conjugate,
     w = uvw[:, :, 2:3] * inv_wl
     hx, hy, fx, fy, fz = coordinates(u, v, w, X, os_, osw, theta, wstep)
     ok = (hx > half) & (hx < X - half) & (hy > half) & (hy < Y - half)
+    # w-kernel rows past the table (negative ioz, reference reads out of
+    # bounds): left unwritten, as the HIP kernel does.
+    ok &= fz < osw
     t_i, b_i, c_i = np.nonzero(ok)
     hx, hy = hx[ok], hy[ok]
     ku = uv_kernel[fx[ok]]            # [n, K]
@@ -92,6 +95,8 @@ def degrid_loops(grid, uvw, uv_kernel, w_kernel, theta, wstep, f0, df,
                 fy = os_ - 1 - cmod(ioy, os_)
                 fz = osw - 1 - cmod(ioz, osw)
                 if not (half < hx < X - half and half < hy < Y - half):
+                    continue
+                if fz >= osw:
                     continue
                 for p in range(P):
                     acc = 0j

@@ -64,6 +64,10 @@ __global__ __launch_bounds__(64 * kWaves) void k_degrid_custom(CParams p,
     if (!(home_x > half && home_x < p.X - half && home_y > half &&
             home_y < p.Y - half))
         return;
+    // A negative ioz that is not a multiple of osw gives a w-kernel row past
+    // the table, which the reference reads out of bounds (undefined); such
+    // visibilities are left unwritten, like those off the grid.
+    if (frac_z >= osw) return;
     const double* ku = uv_kernel + (int64_t)p.K * frac_x;
     const double* kv = uv_kernel + (int64_t)p.K * frac_y;
     const double* kw = w_kernel + (int64_t)p.KW * frac_z;

@@ -19,10 +19,14 @@ REF = dict(theta=0.1, wstep=250.0, f0=100e6, df=0.1e6)
 
 
 def make_case(T=4, B=14, C=5, P=1, X=512, Z=4, K=8, KW=4, os_=16000,
-              seed=2, spread=1.0):
+              seed=2, spread=1.0, w_neg=0.0):
     rng = np.random.default_rng(seed)
     grid = rng.random((C, Z, X, X, P)) + 1j * rng.random((C, Z, X, X, P))
     uvw = spread * rng.random((T, B, 3))
+    # w_neg > 0: odd baselines get w down to -w_neg metres, some below
+    # -wstep, whose w-kernel rows fall outside the table (left unwritten).
+    if w_neg > 0:
+        uvw[:, 1::2, 2] = -w_neg * rng.random((T, B // 2))
     uv_kernel = rng.random((os_, K))
     w_kernel = rng.random((os_, KW))
     return grid, uvw, uv_kernel, w_kernel
@@ -38,6 +42,15 @@ def test_oracle_vectorised_matches_loops():
     do.degrid(*args, False, a)
     do.degrid_loops(*args, False, b)
     assert np.count_nonzero(a == 9 + 9j) > 0          # some off the grid
+    np.testing.assert_allclose(a, b, rtol=1e-13)
+    grid, uvw, ku, kw = make_case(T=2, B=6, C=3, P=1, X=64, os_=64,
+                                  w_neg=3000.0, seed=5)
+    a = np.full((2, 6, 3, 1), 9 + 9j)
+    b = a.copy()
+    args = (grid, uvw, ku, kw, 0.01, 250.0, 100e6, 0.1e6)
+    do.degrid(*args, False, a)
+    do.degrid_loops(*args, False, b)
+    assert np.count_nonzero(a[:, 1::2] == 9 + 9j) > 0   # w rows off table
     np.testing.assert_allclose(a, b, rtol=1e-13)
     do.degrid(*args, True, a)
     do.degrid_loops(*args, True, b)
@@ -68,7 +81,9 @@ def test_library_exports_degrid_custom():
 def test_gpu_matches_oracle(device, on_device, P, conj):
     from ska_sdp_func.grid_data import degrid_uvw_custom
     for kw_args in (dict(P=P), dict(P=P, X=128, os_=64, spread=4000.0,
-                                    T=8, B=40)):
+                                    T=8, B=40),
+                    dict(P=P, X=128, os_=64, spread=4000.0, T=8, B=40,
+                         w_neg=2500.0)):
         grid, uvw, ku, kw = make_case(**kw_args)
         shape = uvw.shape[:2] + (grid.shape[0], P)
         ref = np.full(shape, 5 - 5j)
