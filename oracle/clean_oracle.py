@@ -16,10 +16,10 @@ Follows src/ska-sdp-func/clean/sdp_hogbom_clean.cpp of ska-sdp-func 1.2.2
                          (scipy.signal.convolve mode="same"), rounded to T,
                          plus the residual in T.
 
-Parity pinning: the reference's own test (tests/clean/test_hogbom_clean.py)
+Parity unpinned against reference outputs: the reference's own test (tests/clean/test_hogbom_clean.py)
 builds its dirty image with the cupy-only gridder path and compares against
 a Python CLEAN at 6 / 4 decimals; it holds no golden vectors. This
-restatement is pinned by a known answer (a delta PSF: the component map
+restatement is checked by a known answer (a delta PSF: the component map
 and residual follow g f (1 - g)^k exactly, the stop cycle is predictable)
 and by the "same" alignment checked against scipy.signal.convolve.
 """

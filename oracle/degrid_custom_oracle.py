@@ -6,6 +6,11 @@ Restates src/ska-sdp-func/grid_data/sdp_degrid_uvw_custom.cpp (ska-sdp-func
 in-grid test :134-140, the nested x / y / z sums :143-176 in that order,
 conjugation :177, output only for in-grid visibilities. A vectorised form
 (numpy over visibilities) and a plain-loop form for tiny inputs.
+
+Parity unpinned against reference outputs: the reference's tests for
+this function hold no golden vectors and running reference code is
+denied; checked against the plain-loop form and analytic
+known answers (tests/).
 """
 import numpy as np
 

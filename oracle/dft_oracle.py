@@ -9,9 +9,9 @@ The phasor is rounded to the visibility precision (complex<VIS_TYPE>(cos,
 sin)), fluxes are cast to it, and the polarisations accumulate over the
 components in order in that precision.
 
-Parity pinning: the reference test (tests/visibility/test_dft.py) compares
+Parity unpinned against reference outputs: the reference test (tests/visibility/test_dft.py) compares
 its CPU and GPU paths with each other and holds no golden vectors; this
-restatement is pinned by its loop form (dft_loops, the reference loop nest
+restatement is checked by its loop form (dft_loops, the reference loop nest
 written out scalar by scalar) and by known answers (a source at the phase
 centre returns its flux, a source at l = 1 gives exp(-2 pi i u)).
 """
