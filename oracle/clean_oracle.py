@@ -77,3 +77,71 @@ def hogbom_clean(dirty, psf, details, loop_gain, threshold, cycle_limit):
         cycles += 1
     sky = restore(model, cbeam(details, T), res)
     return model, res, sky, cycles
+
+
+# Multi-scale CLEAN (src/ska-sdp-func/clean/sdp_ms_clean_cornwell.cpp,
+# CPU path, ska-sdp-func 1.2.2).
+
+def conv_same(a, b):
+    """sdp_fft_convolution (sdp_fft_convolution.cpp:127-244): linear
+    convolution "same"-aligned to a, out[i] = sum_k a[k] b[i - k +
+    (n_b - 1) // 2], by FFT in a's precision."""
+    import scipy.signal
+    return scipy.signal.fftconvolve(a, b, mode="same").astype(a.dtype)
+
+
+def scale_kernel(scale, size, dtype):
+    """:111-166: a delta at (size/2, size/2) for scale 0, else
+    exp(-d^2 / (2 s^2)) / (pi 2 s^2) with s = 3/16 scale, rounded to T."""
+    T = np.dtype(dtype).type
+    c = size // 2
+    k = np.zeros((size, size), dtype)
+    if scale == 0:
+        k[c, c] = 1
+        return k
+    sigma = T((3.0 / 16.0) * scale)
+    tss = T(2.0 * float(sigma) * float(sigma))
+    x = (np.arange(size) - c).astype(np.int64)
+    d = (x[:, None] * x[:, None] + x[None, :] * x[None, :]).astype(np.float64)
+    return (np.exp(-d / float(tss)) / (np.pi * float(tss))).astype(dtype)
+
+
+def ms_clean_cornwell(dirty, psf, details, scales, loop_gain, threshold,
+                      cycle_limit):
+    """Returns (clean_model, residual, skymodel, cycles) in dirty's type."""
+    T = dirty.dtype.type
+    n, L = dirty.shape[0], psf.shape[0]
+    S = len(scales)
+    kern = [scale_kernel(int(s), L, dirty.dtype) for s in scales]
+    beam = cbeam([details[0], details[1], details[2], L],
+                 dirty.dtype).astype(dirty.dtype)          # .cpp:401
+    spsf = [[conv_same(conv_same(psf, kern[a]), kern[b]) for b in range(S)]
+            for a in range(S)]                               # :414-486
+    res = [conv_same(dirty, kern[a]) for a in range(S)]    # :488-515
+    coupling = [T(max(0.0, float(spsf[a][a].max()))) for a in range(S)]
+    comp = np.zeros_like(dirty)
+    g, thr = T(loop_gain), T(threshold)
+    cycles = 0
+    while cycles < cycle_limit:                              # :557-702
+        peak, idx = [], []
+        for a in range(S):
+            k = int(np.argmax(res[a]))
+            ok = res[a].flat[k] > 0
+            peak.append(res[a].flat[k] if ok else T(0))
+            idx.append(k if ok else 0)
+        m, mb = 0, T(0)
+        for a in range(S):
+            biased = T(peak[a]) / coupling[a]
+            if biased > mb:
+                m, mb = a, biased
+        if res[m].flat[idx[m]] < thr:
+            break
+        gm = T(g * mb)
+        x, y = divmod(idx[m], n)
+        x0, y0 = n - x, n - y
+        comp = comp + gm * kern[m][x0:x0 + n, y0:y0 + n]
+        for a in range(S):
+            res[a] = res[a] - gm * spsf[a][m][x0:x0 + n, y0:y0 + n]
+        cycles += 1
+    sky = conv_same(comp, beam) + res[0]                    # :704-749
+    return comp, res[0], sky, cycles

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--sizes", type=int, nargs="+", default=[256, 1024, 2048])
     ap.add_argument("--cycles", type=int, default=5000)
     ap.add_argument("--cpu-cycles", type=int, default=200)
+    ap.add_argument("--ms", action="store_true",
+                    help="also time multi-scale CLEAN (5 scales, f64)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     beam = np.array([2.0, 2.0, 1.0, 128.0])
@@ -53,6 +55,34 @@ def main():
                 tc = time.perf_counter() - t0
                 row["cpu_oracle_us_per_cycle"] = round(1e6 * tc / args.cpu_cycles, 1)
             print(json.dumps(row), flush=True)
+    if args.ms:
+        from ska_sdp_func.clean import ms_clean_cornwell
+        scales = np.array([0, 2, 4, 8, 16], dtype=np.intc)
+        for n in (256, 1024):
+            psf64 = uv_psf(n, nbl=200)
+            dirty64 = point_dirty(psf64, n)
+            d = torch.from_numpy(dirty64).to(dev)
+            p = torch.from_numpy(psf64).to(dev)
+            outs = [torch.zeros((n, n), dtype=torch.float64, device=dev)
+                    for _ in range(3)]
+            ms_clean_cornwell(d, p, beam, scales, 0.1, -1e30, 1, *outs)
+            torch.cuda.synchronize()              # warm-up (FFT plans)
+            t0 = time.perf_counter()
+            ms_clean_cornwell(d, p, beam, scales, 0.1, -1e30, 1, *outs)
+            torch.cuda.synchronize()
+            t_setup = time.perf_counter() - t0    # set-up + one cycle
+            t0 = time.perf_counter()
+            ms_clean_cornwell(d, p, beam, scales, 0.1, -1e30, args.cycles,
+                              *outs)
+            torch.cuda.synchronize()
+            t = time.perf_counter() - t0
+            print(json.dumps({"function": "ms_clean_cornwell", "n": n,
+                              "scales": 5, "dtype": "float64",
+                              "cycles": args.cycles, "s": round(t, 4),
+                              "setup_s": round(t_setup, 4),
+                              "us_per_cycle": round(
+                                  1e6 * (t - t_setup) / args.cycles, 2)}),
+                  flush=True)
 
 
 if __name__ == "__main__":

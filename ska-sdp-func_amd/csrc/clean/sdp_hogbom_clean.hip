@@ -36,21 +36,19 @@
 
 #include "ska-sdp-func/clean/sdp_hogbom_clean.h"
 #include "../utility/sdp_hip.h"
+#include "clean_common.h"
 
 namespace {
 
-constexpr int kThreads = 256;
+using sdp_clean::kThreads;
+using sdp_clean::kWaves;
+using sdp_clean::Peak;
+using sdp_clean::better;
+using sdp_clean::block_best;
 constexpr int kPix = 4;                    // residual pixels per thread
 constexpr int kSpan = kThreads * kPix;     // pixels per workgroup
-constexpr int kWaves = kThreads / 64;
 constexpr int kTile = 16;                  // restore tile edge
 constexpr int kSyncEvery = 64;             // cycles between stop checks
-
-struct Peak
-{
-    double v;
-    long long i;
-};
 
 struct CleanState
 {
@@ -59,53 +57,6 @@ struct CleanState
     int done;          // stop flag (below threshold / nothing left)
     int cycles;        // cycles performed
 };
-
-// Larger value wins; ties go to the lower flat index (first maximum).
-__device__ __forceinline__ bool better(double v, long long i, double bv,
-        long long bi)
-{
-    return v > bv || (v == bv && i < bi);
-}
-
-__device__ __forceinline__ void wave_best(double& v, long long& i)
-{
-    for (int o = 32; o > 0; o >>= 1)
-    {
-        const double ov = __shfl_xor(v, o, 64);
-        const long long oi = __shfl_xor(i, o, 64);
-        if (better(ov, oi, v, i))
-        {
-            v = ov;
-            i = oi;
-        }
-    }
-}
-
-// Result valid in thread 0.
-__device__ __forceinline__ void block_best(double& v, long long& i)
-{
-    __shared__ double s_v[kWaves];
-    __shared__ long long s_i[kWaves];
-    wave_best(v, i);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0)
-    {
-        s_v[w] = v;
-        s_i[w] = i;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0)
-    {
-        for (int k = 1; k < kWaves; ++k)
-        {
-            if (better(s_v[k], s_i[k], v, i))
-            {
-                v = s_v[k];
-                i = s_i[k];
-            }
-        }
-    }
-}
 
 template<typename T>
 struct CleanArgs
@@ -233,14 +184,8 @@ __global__ void k_cbeam(double* cb, int nb, double sx, double sy,
 {
     const int i = blockIdx.x * kThreads + threadIdx.x;
     if (i >= nb * nb) return;
-    const double th = (M_PI / 180) * theta_deg;
-    const double ct = cos(th), st = sin(th), s2 = sin(2 * th);
-    const double a = ct * ct / (2 * sx * sx) + st * st / (2 * sy * sy);
-    const double b = s2 / (4 * sx * sx) - s2 / (4 * sy * sy);
-    const double c = st * st / (2 * sx * sx) + ct * ct / (2 * sy * sy);
-    const int x = i / nb, y = i % nb, c0 = nb / 2;
-    const double dx = x - c0, dy = y - c0;
-    cb[i] = (double)(T)exp(-(a * dx * dx + 2 * b * dx * dy + c * dy * dy));
+    cb[i] = (double)(T)sdp_clean::cbeam_value(i / nb, i % nb, nb, sx, sy,
+            theta_deg);
 }
 
 template<typename T>
