@@ -9,8 +9,14 @@
 // coalesced load each) and every thread accumulates its visibility's
 // polarisations in registers over the chunk. The phase and phasor follow
 // sdp_dft.cpp:49-77 (v00) and :291-318 (v01) operation for operation.
+// v01 by default takes k_dft_rec (below): one thread per (time, baseline)
+// and 8 channels, the phasor advanced across channels by a complex
+// multiplication instead of a sincos per channel, and the flux products
+// accumulated with fused multiply-adds (as the reference's CUDA build
+// contracts them); within 1e-12 (c128) of the CPU path.
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 
 #include "ska-sdp-func/visibility/sdp_dft.h"
 #include "../utility/sdp_hip.h"
@@ -96,6 +102,104 @@ __global__ __launch_bounds__(kThreads) void k_dft(DftArgs a,
         z.x = acc_re[q];
         z.y = acc_im[q];
         out[q] = z;
+    }
+}
+
+// v01 with a channel recurrence. The phase is linear in the channel index
+// (inv_wavelength = (f0 + c df) / c0), so a thread owns one (time,
+// baseline) and kCb consecutive channels: per component it evaluates the
+// phasor of the first channel exactly as the reference (one sincos of the
+// reference's phase) and one sincos of the per-channel step, then advances
+// the phasor by complex multiplication in double (kCb - 1 steps, a few ulp
+// from the reference's per-channel sincos). Components and their fluxes
+// for the thread's channels are staged through LDS, 64 at a time.
+constexpr int kCb = 8;
+constexpr int kSrcChunk = 64;
+
+template<typename V>
+__global__ __launch_bounds__(kThreads) void k_dft_rec(DftArgs a,
+        typename Cx2<V>::type* __restrict__ vis)
+{
+#pragma clang fp contract(off)
+    using C2 = typename Cx2<V>::type;
+    __shared__ double s_dir[kSrcChunk][3];
+    __shared__ double2 s_flux[kSrcChunk][kCb][4];
+    const int64_t b = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+    const int64_t c0 = (int64_t)blockIdx.y * kCb, t = blockIdx.z;
+    const int nc = (int)min((int64_t)kCb, a.C - c0);
+    const bool live = b < a.B;
+    double uu = 0.0, vv = 0.0, ww = 0.0;
+    if (live)
+    {
+        const double* p = a.uvw + (t * a.B + b) * 3;
+        uu = p[0];
+        vv = p[1];
+        ww = p[2];
+    }
+    const double inv_wl0 = (a.f0 + c0 * a.df) / kC0;
+    const double dinv_wl = a.df / kC0;
+    V acc_re[kCb][4], acc_im[kCb][4];
+#pragma unroll
+    for (int j = 0; j < kCb; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc_re[j][q] = acc_im[j][q] = (V)0;
+    const int per_src = nc * (int)a.P;
+    for (int64_t s0 = 0; s0 < a.S; s0 += kSrcChunk)
+    {
+        const int n = (int)min((int64_t)kSrcChunk, a.S - s0);
+        __syncthreads();
+        for (int k = threadIdx.x; k < n * 3; k += kThreads)
+            s_dir[k / 3][k % 3] = a.dir[3 * s0 + k];
+        for (int k = threadIdx.x; k < n * per_src; k += kThreads)
+        {
+            const int src = k / per_src, r = k - src * per_src;
+            const int j = r / (int)a.P, q = r - j * (int)a.P;
+            s_flux[src][j][q] = a.flux[((s0 + src) * a.C + c0 + j) * a.P + q];
+        }
+        __syncthreads();
+        if (!live) continue;
+        for (int k = 0; k < n; ++k)
+        {
+            const double l = s_dir[k][0], m = s_dir[k][1], nn = s_dir[k][2];
+            const double dot = l * uu + m * vv + nn * ww;
+            double sn, cs, dsn, dcs;
+            sincos(-2.0 * M_PI * inv_wl0 * dot, &sn, &cs);
+            sincos(-2.0 * M_PI * dinv_wl * dot, &dsn, &dcs);
+#pragma unroll
+            for (int j = 0; j < kCb; ++j)
+            {
+                if (j >= nc) break;
+                const V pr = (V)cs, pi = (V)sn;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                {
+                    if (q >= a.P) break;
+                    const V fr = (V)s_flux[k][j][q].x;
+                    const V fi = (V)s_flux[k][j][q].y;
+                    acc_re[j][q] = fma(-pi, fi, fma(pr, fr, acc_re[j][q]));
+                    acc_im[j][q] = fma(pi, fr, fma(pr, fi, acc_im[j][q]));
+                }
+                const double ncs = cs * dcs - sn * dsn;
+                sn = cs * dsn + sn * dcs;
+                cs = ncs;
+            }
+        }
+    }
+    if (!live) return;
+#pragma unroll
+    for (int j = 0; j < kCb; ++j)
+    {
+        if (j >= nc) break;
+        C2* out = vis + ((t * a.B + b) * a.C + c0 + j) * a.P;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+        {
+            if (q >= a.P) break;
+            C2 z;
+            z.x = acc_re[j][q];
+            z.y = acc_im[j][q];
+            out[q] = z;
+        }
     }
 }
 
@@ -224,8 +328,19 @@ void dft(const sdp_Mem* dir, const sdp_Mem* flux, const sdp_Mem* uvw,
     {
         const dim3 grid((unsigned)((a.B + kThreads - 1) / kThreads),
                 (unsigned)a.C, (unsigned)a.T);
+        const dim3 grid_rec(grid.x, (unsigned)((a.C + kCb - 1) / kCb),
+                (unsigned)a.T);
         const bool dbl = sdp_mem_type(vis) == SDP_MEM_COMPLEX_DOUBLE;
-        if (v01 && dbl)
+        // SDP_DFT_RECURRENCE=0: one sincos per channel (A/B measurement).
+        static const bool rec = [] {
+            const char* e = std::getenv("SDP_DFT_RECURRENCE");
+            return !(e && e[0] == '0');
+        }();
+        if (v01 && rec && dbl)
+            k_dft_rec<double><<<grid_rec, kThreads>>>(a, (double2*)out);
+        else if (v01 && rec)
+            k_dft_rec<float><<<grid_rec, kThreads>>>(a, (float2*)out);
+        else if (v01 && dbl)
             k_dft<double, true><<<grid, kThreads>>>(a, (double2*)out);
         else if (v01)
             k_dft<float, true><<<grid, kThreads>>>(a, (float2*)out);
