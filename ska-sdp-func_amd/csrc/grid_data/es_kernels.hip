@@ -964,7 +964,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     // Per-wave visit lists: wave w, column block c holds the chunk's
     // entries whose taps touch sub-tile (w, c), in entry order.
     __shared__ uint16_t s_list[4][4][kChunk];
-    __shared__ uint32_t s_info[kChunk];        // packed entry + hit masks
+    // Packed entry + hit masks; slot kChunk is the padding visit, whose
+    // offsets put every lane's tap index out of range (zero taps).
+    __shared__ uint32_t s_info[kChunk + 1];
     // Tap tables; the extra last element of each is a zero that masked
     // lanes read instead of branching around the load.
     constexpr int kZero = kChunk * NTAP;
@@ -999,6 +1001,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     {
         s_ku[kZero] = 0.0f;
         s_kv[kZero] = make_float2(0.0f, 0.0f);
+        s_info[kChunk] = 255u << 8 | 255u << 16;
     }
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rw = r;
@@ -1078,14 +1081,26 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 lcnt[cblk] += (int)__popcll(m);
             }
         }
+        // Pad every list to a multiple of 16 visits with the padding visit,
+        // so the matrix loop needs no bounds checks.
+#pragma unroll
+        for (int cblk = 0; cblk < 4; ++cblk)
+        {
+            const int pad = ((lcnt[cblk] + 15) & ~15) - lcnt[cblk];
+            if (lane < pad) s_list[wave][cblk][lcnt[cblk] + lane] = kChunk;
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int cblk = 0; cblk < 4; ++cblk)
         {
-            const int cnt = __builtin_amdgcn_readfirstlane(lcnt[cblk]);
+            const int cnt = __builtin_amdgcn_readfirstlane(
+                    (lcnt[cblk] + 15) & ~15);
             const uint16_t* list = s_list[wave][cblk];
             const int base_v = cblk * 16 + i + 32;
+            // The loop carries only this block's two accumulators (keeps
+            // the register allocator from rotating the AGPRs of all four).
+            f32x4 re = acc_re[cblk], im = acc_im[cblk];
             // Four groups of four visits per step: all LDS reads of a step
             // are issued before the first matrix op waits on them.
             for (int g = 0; g < cnt; g += 16)
@@ -1093,7 +1108,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 uint32_t q[4];
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
-                    q[s] = s_info[list[min(g + 4 * s + kq, cnt - 1)]];
+                    q[s] = s_info[list[g + 4 * s + kq]];
                 float a[4];
                 float2 bb[4];
 #pragma unroll
@@ -1102,25 +1117,27 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                     const int e = (int)(q[s] & 0xffu);
                     const int du = base_u - (int)((q[s] >> 8) & 0xffu);
                     const int dv = base_v - (int)((q[s] >> 16) & 0xffu);
-                    const bool valid = g + 4 * s + kq < cnt;
-                    const int ia = (valid && (unsigned)du < (unsigned)NTAP) ?
+                    const int ia = ((unsigned)du < (unsigned)NTAP) ?
                             e * NTAP + du : kZero;
                     const int ib = ((unsigned)dv < (unsigned)NTAP) ?
                             e * NTAP + dv : kZero;
                     a[s] = s_ku[ia];
                     bb[s] = s_kv[ib];
                 }
-                // Groups past cnt multiply zeros (a = 0): no branch, so
-                // the loads above stay batched ahead of the matrix ops.
+                // Each chain back to back (same-accumulator MFMAs forward
+                // their result); interleaving re / im made the register
+                // allocator swap the two accumulators every iteration.
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
-                {
-                    acc_re[cblk] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s],
-                            bb[s].x, acc_re[cblk], 0, 0, 0);
-                    acc_im[cblk] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s],
-                            bb[s].y, acc_im[cblk], 0, 0, 0);
-                }
+                    re = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bb[s].x,
+                            re, 0, 0, 0);
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                    im = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bb[s].y,
+                            im, 0, 0, 0);
             }
+            acc_re[cblk] = re;
+            acc_im[cblk] = im;
         }
         r = rn;
         rw = rwn;
