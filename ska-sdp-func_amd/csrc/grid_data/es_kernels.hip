@@ -377,12 +377,19 @@ __global__ __launch_bounds__(NT) void k_bucket_fill(EsParams<T> p,
     const int64_t r0 = (int64_t)blockIdx.x * chunk;
     const int64_t r1 = min(num_rows, r0 + chunk);
     const int half = p.G / 2;
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += NT)
+    // Threads walk the chunk's visibilities in memory order (consecutive
+    // lanes = consecutive channels of a row), so the vis / weight loads of
+    // a wave are coalesced for any channel count; the row's uvw is an L1
+    // hit shared by its channels.
+    const uint32_t nvis = (uint32_t)((r1 - r0) * num_chan);
+    for (uint32_t li = threadIdx.x; li < nvis; li += NT)
     {
-        const T u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2];
-        for (int c = 0; c < num_chan; ++c)
+        const uint32_t rl = num_chan == 1 ? li : li / (uint32_t)num_chan;
+        const int c = (int)(li - rl * (uint32_t)num_chan);
+        const int64_t r = r0 + rl;
+        const int64_t i = r * num_chan + c;
         {
-            const int64_t i = r * num_chan + c;
+            const T u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2];
             Footprint<T> f;
             if (!footprint(p, u, v, w, freq[c], f)) continue;
             T rec[kWords];
