@@ -2,6 +2,8 @@
 
 from .dft import dft_point_v00, dft_point_v01
 from .flagger import flagger_dynamic_threshold
+from .tiled_functions import (bucket_sort, count_and_prefix_sum,
+                              tiled_indexing)
 from .weighting import briggs_weights, get_uv_range, uniform_weights
 
 __all__ = [
@@ -11,4 +13,7 @@ __all__ = [
     "briggs_weights",
     "get_uv_range",
     "uniform_weights",
+    "bucket_sort",
+    "count_and_prefix_sum",
+    "tiled_indexing",
 ]
