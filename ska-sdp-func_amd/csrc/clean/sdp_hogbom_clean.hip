@@ -561,6 +561,7 @@ extern "C" void sdp_hogbom_clean(const sdp_Mem* dirty_img, const sdp_Mem* psf,
         return;
     }
     const int64_t n = sdp_mem_shape_dim(dirty_img, 0);
+    if (n == 0) return;              // empty images: nothing to clean
     const bool dbl = sdp_mem_type(dirty_img) == SDP_MEM_DOUBLE;
     const size_t esz = dbl ? 8 : 4;
     const size_t img_bytes = (size_t)n * n * esz;
