@@ -799,8 +799,13 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
     // blocks (acc64 = acc64 / D^kDftBlock + acc32): the reference keeps
     // wimg in complex double; the block partial sums carry the f32
     // rounding of kDftBlock steps, like its complex-float layers.
+    // The f32 block partial lives in the matrix-core accumulators: each
+    // layer first scales it by 1 / D, then the layer's rank update is
+    // accumulated onto it (no zeroing / read-back of a separate layer sum).
     Cx<double> acc[4], dinv_k[4];
-    float2 acc32[4], dinv32[4];
+    float2 dinv32[4];
+    f32x4 a_re = {0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 a_im = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int r = 0; r < 4; ++r)
     {
@@ -809,7 +814,6 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
         const Cx<double> di = d.wp_inv[e];
         dinv32[r] = make_float2((float)di.re, (float)di.im);
         dinv_k[r] = cpow_int(di, kDftBlock);
-        acc32[r] = make_float2(0.0f, 0.0f);
     }
     Cx<float>* out = d.out + (int64_t)slot * S * S;
     if (n <= 0)
@@ -850,8 +854,15 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
     {
         const int lo = s_start[max(0, min(npl, L - ws + 1 - P_first))];
         const int hi = s_start[max(0, min(npl, L + 1 - P_first))];
-        f32x4 c_re = {0.0f, 0.0f, 0.0f, 0.0f};
-        f32x4 c_im = {0.0f, 0.0f, 0.0f, 0.0f};
+        // wimg = wimg / D (f32 within the block), then + layer below.
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const float xr = a_re[r], xi = a_im[r];
+            const float2 q = dinv32[r];
+            a_re[r] = xr * q.x - xi * q.y;
+            a_im[r] = xr * q.y + xi * q.x;
+        }
         for (int a = lo; a < hi; a += kDftCap)
         {
             const int b = min(hi, a + kDftCap);
@@ -961,23 +972,15 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                 const float2 bv = s_kv[rs][bm + i];
                 const float kw = ok ? s_kw[rs][L & 15] : 0.0f;
                 const float ar = av.x * kw, ai = av.y * kw;
-                c_re = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.x, c_re,
+                a_re = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.x, a_re,
                         0, 0, 0);
-                c_re = __builtin_amdgcn_mfma_f32_16x16x4f32(-ai, bv.y, c_re,
+                a_re = __builtin_amdgcn_mfma_f32_16x16x4f32(-ai, bv.y, a_re,
                         0, 0, 0);
-                c_im = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.y, c_im,
+                a_im = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.y, a_im,
                         0, 0, 0);
-                c_im = __builtin_amdgcn_mfma_f32_16x16x4f32(ai, bv.x, c_im,
+                a_im = __builtin_amdgcn_mfma_f32_16x16x4f32(ai, bv.x, a_im,
                         0, 0, 0);
             }
-        }
-        // wimg = wimg / D + layer (f32 within the block).
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-        {
-            const float2 a = acc32[r], q = dinv32[r];
-            acc32[r] = make_float2(a.x * q.x - a.y * q.y + c_re[r],
-                    a.x * q.y + a.y * q.x + c_im[r]);
         }
         if ((L - L_first + 1 + blk_off) % kDftBlock == 0)
         {
@@ -985,11 +988,12 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
             for (int r = 0; r < 4; ++r)
             {
                 Cx<double> z = cmul(acc[r], dinv_k[r]);
-                z.re += (double)acc32[r].x;
-                z.im += (double)acc32[r].y;
+                z.re += (double)a_re[r];
+                z.im += (double)a_im[r];
                 acc[r] = z;
-                acc32[r] = make_float2(0.0f, 0.0f);
             }
+            a_re = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            a_im = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         }
     }
     // End of tower: wimg * D^(L_last - w_support / 2) (.cpp:1102-1113),
