@@ -1039,9 +1039,12 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     __shared__ float2 s_tw[kDftMaxS];
     __shared__ int s_start[kDftLayers + 1];
-    __shared__ float2 s_ku[kDftCap][kDftTile];      // conj KU(l), tile rows
-    __shared__ float2 s_kv[kDftCap][kDftTile];      // conj KV(m), tile cols
-    __shared__ float s_kw[kDftCap][16];             // keyed by w-layer % 16
+    // Rows padded by 2 float2: a lane reads 4 consecutive entries of its
+    // visibility's row (two 16-byte LDS reads) and the 16 lanes of a
+    // quarter-wave, on 16 different rows, then cover all 64 banks once.
+    __shared__ float2 s_ku[kDftCap][kDftTile + 2];  // conj KU(l), tile rows
+    __shared__ float2 s_kv[kDftCap][kDftTile + 2];  // conj KV(m), tile cols
+    __shared__ float s_kw[kDftCap][17];             // keyed by w-layer % 16
     __shared__ int s_tap[kDftCap][5];
     __shared__ int s_P[kDftCap];
     __shared__ float s_kuv[kDftCap][32];
@@ -1067,14 +1070,17 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
     const int npl = P_last - P_first + 1;
     const int L_first = P_first, L_last = P_last + ws - 1;
 
-    // A-operand pixels of this lane: row bl + i, columns bm + 4 kk + kq.
+    // A-operand pixels of this lane: row bl + i, columns bm + 4 kq + kk
+    // (MFMA kk takes its k = kq from column bm + 4 kq + kk; any bijection
+    // of the 16 columns works as long as A and B share it, and this one
+    // puts a lane's 4 B entries next to each other in LDS).
     Cx<double> y64[4], dinv_k[4];
     float2 y32[4], dinv32[4];
     const Cx<float>* X = d.in + (int64_t)slot * S * S;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk)
     {
-        const int64_t e = (int64_t)(L0 + bl + i) * S + (M0 + bm + 4 * kk + kq);
+        const int64_t e = (int64_t)(L0 + bl + i) * S + (M0 + bm + 4 * kq + kk);
         const Cx<float> x = X[e];
         y64[kk] = cmul(cx<double>((double)x.re, (double)x.im),
                 cpow_int(d.wp[e], -(L_first - ws / 2)));
@@ -1215,16 +1221,15 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
             {
                 const int v = c16 + i;
                 const bool ok = v < b;
+                // Column i of T only sees column i of B: a lane past the
+                // window reads a staged row and its result is dropped below.
                 const int rs = (ok ? v : a) % kDftCap;
                 f32x4 t_re = {0.0f, 0.0f, 0.0f, 0.0f};
                 f32x4 t_im = {0.0f, 0.0f, 0.0f, 0.0f};
                 float2 bv[4];
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk)
-                {
-                    bv[kk] = s_kv[rs][bm + 4 * kk + kq];
-                    if (!ok) bv[kk] = make_float2(0.0f, 0.0f);
-                }
+                    bv[kk] = s_kv[rs][bm + 4 * kq + kk];
 #pragma unroll
                 for (int kk = 0; kk < 4; ++kk)
                 {
@@ -1244,8 +1249,10 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
                 for (int r = 0; r < 4; ++r)
                 {
                     const float2 ku = s_ku[rs][bl + 4 * kq + r];
-                    pr += ku.x * t_re[r] - ku.y * t_im[r];
-                    pi += ku.x * t_im[r] + ku.y * t_re[r];
+                    pr = __builtin_fmaf(ku.x, t_re[r], pr);
+                    pr = __builtin_fmaf(-ku.y, t_im[r], pr);
+                    pi = __builtin_fmaf(ku.x, t_im[r], pi);
+                    pi = __builtin_fmaf(ku.y, t_re[r], pi);
                 }
                 pr += __shfl_xor(pr, 16);
                 pi += __shfl_xor(pi, 16);
