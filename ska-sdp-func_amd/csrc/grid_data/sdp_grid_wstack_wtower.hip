@@ -933,7 +933,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                         // e^{2 pi i a l / S} for a = a0, a0 + 1, ...: the
                         // table index advances by l (mod S) per tap and the
                         // checkerboard sign (-1)^(a + l) alternates.
-                        int idx = (int)(((int64_t)a0 * l) % S);
+                        int idx = (int)((uint32_t)(a0 * l) % (uint32_t)S);  // a0, l < S
                         bool neg = (a0 + l) & 1;
                         float sr = 0.0f, si = 0.0f;
                         for (int du = 0; du < W; ++du)
@@ -1196,7 +1196,7 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
                         const int a0 = row ? iu0 : s_tap[rs][1];
                         const float* kt = s_kuv[rs] + (row ? 0 : W);
                         const int l = row ? L0 + q : M0 + q - kDftTile;
-                        int idx = (int)(((int64_t)a0 * l) % S);
+                        int idx = (int)((uint32_t)(a0 * l) % (uint32_t)S);  // a0, l < S
                         bool neg = (a0 + l) & 1;
                         float sr = 0.0f, si = 0.0f;
                         for (int du = 0; du < W; ++du)
