@@ -930,21 +930,22 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                         const int a0 = row ? iu0 : s_tap[rs][1];
                         const float* kt = s_kuv[rs] + (row ? 0 : W);
                         const int l = row ? L0 + q : M0 + q - kDftTile;
-                        // e^{2 pi i a l / S} for a = a0, a0 + 1, ...: the
-                        // table index advances by l (mod S) per tap and the
-                        // checkerboard sign (-1)^(a + l) alternates.
-                        int idx = (int)((uint32_t)(a0 * l) % (uint32_t)S);  // a0, l < S
-                        bool neg = (a0 + l) & 1;
+                        // (-1)^(a + l) e^{2 pi i a l / S} = e^{2 pi i k / S}
+                        // with k = a l + (a + l) S / 2 (mod S; S is even):
+                        // for a = a0, a0 + 1, ... the table index advances
+                        // by l + S / 2 per tap, the checkerboard included.
+                        const uint32_t us = (uint32_t)S;   // a0, l < S
+                        int idx = (int)(((uint32_t)(a0 * l) +
+                                (uint32_t)((a0 + l) & 1) * (us / 2)) % us);
+                        const int step = (int)(((uint32_t)l + us / 2) % us);
                         float sr = 0.0f, si = 0.0f;
                         for (int du = 0; du < W; ++du)
                         {
                             const float2 e = s_tw[idx];
-                            const float kk = neg ? -kt[du] : kt[du];
-                            sr += kk * e.x;
-                            si += kk * e.y;
-                            idx += l;
+                            sr = __builtin_fmaf(kt[du], e.x, sr);
+                            si = __builtin_fmaf(kt[du], e.y, si);
+                            idx += step;
                             if (idx >= S) idx -= S;
-                            neg = !neg;
                         }
                         if (row)
                         {
@@ -1196,18 +1197,20 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
                         const int a0 = row ? iu0 : s_tap[rs][1];
                         const float* kt = s_kuv[rs] + (row ? 0 : W);
                         const int l = row ? L0 + q : M0 + q - kDftTile;
-                        int idx = (int)((uint32_t)(a0 * l) % (uint32_t)S);  // a0, l < S
-                        bool neg = (a0 + l) & 1;
+                        // Checkerboard folded into the index as in
+                        // k_tower_dft.
+                        const uint32_t us = (uint32_t)S;   // a0, l < S
+                        int idx = (int)(((uint32_t)(a0 * l) +
+                                (uint32_t)((a0 + l) & 1) * (us / 2)) % us);
+                        const int step = (int)(((uint32_t)l + us / 2) % us);
                         float sr = 0.0f, si = 0.0f;
                         for (int du = 0; du < W; ++du)
                         {
                             const float2 ew = s_tw[idx];
-                            const float kk = neg ? -kt[du] : kt[du];
-                            sr += kk * ew.x;
-                            si += kk * ew.y;
-                            idx += l;
+                            sr = __builtin_fmaf(kt[du], ew.x, sr);
+                            si = __builtin_fmaf(kt[du], ew.y, si);
+                            idx += step;
                             if (idx >= S) idx -= S;
-                            neg = !neg;
                         }
                         res = make_float2(sr, -si);   // conjugate
                     }
