@@ -1113,7 +1113,11 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
     // Adds the partials of staged visibilities [f0, f1) to their scratch
     // rows and clears them (call between barriers). Visibility v is always
     // flushed by thread v % 256, so a scratch entry's read-modify-writes
-    // stay in one thread's program order.
+    // stay in one thread's program order. A visibility is flushed again
+    // only when a window wider than the ring re-stages it; below fl_hi
+    // (the end of everything flushed so far) the entry is added to, above
+    // it stored (the scratch rows start zeroed either way).
+    int fl_hi = 0;
     auto flush = [&](int f0, int f1) {
         for (int v = f0 + ((t - f0) % 256 + 256) % 256; v < f1; v += 256)
         {
@@ -1127,9 +1131,14 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
                 s_acc[w][rs] = make_float2(0.0f, 0.0f);
             }
             float2* dst = d.part + (int64_t)(s0 + v) * ntiles + tile;
-            const float2 old = *dst;
-            *dst = make_float2(old.x + sum.x, old.y + sum.y);
+            if (v < fl_hi)
+            {
+                const float2 old = *dst;
+                sum = make_float2(old.x + sum.x, old.y + sum.y);
+            }
+            *dst = sum;
         }
+        fl_hi = max(fl_hi, f1);
     };
 
     for (int L = L_first; L <= L_last; ++L)
