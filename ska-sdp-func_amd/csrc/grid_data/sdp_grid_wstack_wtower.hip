@@ -742,6 +742,8 @@ constexpr int kDftTile = 32;     // tile edge (pixels)
 constexpr int kDftLayers = 512;  // max w-layers of a sub-grid's tower
 constexpr int kDftMaxS = 1024;
 constexpr int kDftBlock = 8;     // w-layers per f32 recurrence block
+static_assert((kDftCap & (kDftCap - 1)) == 0 && (kDftTile & (kDftTile - 1)) == 0,
+        "ring slots and tile offsets are taken with masks");
 
 struct DftParams
 {
@@ -880,7 +882,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                 lds_sync();   // ring slots free
                 if (t < cnt)
                 {
-                    const int v = x + t, rs = v % kDftCap;
+                    const int v = x + t, rs = v & (kDftCap - 1);
                     const int4 rec = d.vrec[s0 + v];
                     TowerParams q = tp;
                     q.w_plane = (int)(rec.z + d.P0 - tp.off_w);
@@ -903,7 +905,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                 for (int o = t; o < cnt * per; o += 256)
                 {
                     const int v = x + o / per, j = o % per;
-                    const int rs = v % kDftCap;
+                    const int rs = v & (kDftCap - 1);
                     const bool valid = s_tap[rs][0] >= 0;
                     if (j < 2 * W)
                     {
@@ -920,8 +922,8 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                 lds_sync();
                 for (int o = t; o < cnt * 2 * kDftTile; o += 256)
                 {
-                    const int v = x + o / (2 * kDftTile);
-                    const int rs = v % kDftCap, q = o % (2 * kDftTile);
+                    const int v = x + (int)((unsigned)o / (2 * kDftTile));
+                    const int rs = v & (kDftCap - 1), q = o & (2 * kDftTile - 1);
                     const int iu0 = s_tap[rs][0];
                     float2 res = make_float2(0.0f, 0.0f);
                     if (iu0 >= 0)
@@ -968,7 +970,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
             {
                 const int v = c4 + kq;
                 const bool ok = v < b;
-                const int rs = (ok ? v : a) % kDftCap;
+                const int rs = (ok ? v : a) & (kDftCap - 1);
                 const float2 av = s_aku[rs][bl + i];
                 const float2 bv = s_kv[rs][bm + i];
                 const float kw = ok ? s_kw[rs][L & 15] : 0.0f;
@@ -1092,7 +1094,7 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
     }
     for (int k = t; k < S; k += 256) s_tw[k] = d.tw[k];
     for (int k = t; k < 4 * kDftCap; k += 256)
-        s_acc[k / kDftCap][k % kDftCap] = make_float2(0.0f, 0.0f);
+        s_acc[k / kDftCap][k & (kDftCap - 1)] = make_float2(0.0f, 0.0f);
     if (t == 0)
     {
         s_start[0] = 0;
@@ -1121,7 +1123,7 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
     auto flush = [&](int f0, int f1) {
         for (int v = f0 + ((t - f0) % 256 + 256) % 256; v < f1; v += 256)
         {
-            const int rs = v % kDftCap;
+            const int rs = v & (kDftCap - 1);
             float2 sum = make_float2(0.0f, 0.0f);
 #pragma unroll
             for (int w = 0; w < 4; ++w)
@@ -1161,7 +1163,7 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
                 const int cnt = e - x;
                 if (t < cnt)
                 {
-                    const int v = x + t, rs = v % kDftCap;
+                    const int v = x + t, rs = v & (kDftCap - 1);
                     const int4 rec = d.vrec[s0 + v];
                     TowerParams q = tp;
                     q.w_plane = (int)(rec.z + d.P0 - tp.off_w);
@@ -1179,7 +1181,7 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
                 for (int o = t; o < cnt * per; o += 256)
                 {
                     const int v = x + o / per, j = o % per;
-                    const int rs = v % kDftCap;
+                    const int rs = v & (kDftCap - 1);
                     const bool valid = s_tap[rs][0] >= 0;
                     if (j < 2 * W)
                     {
@@ -1196,8 +1198,8 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
                 lds_sync();
                 for (int o = t; o < cnt * 2 * kDftTile; o += 256)
                 {
-                    const int v = x + o / (2 * kDftTile);
-                    const int rs = v % kDftCap, q = o % (2 * kDftTile);
+                    const int v = x + (int)((unsigned)o / (2 * kDftTile));
+                    const int rs = v & (kDftCap - 1), q = o & (2 * kDftTile - 1);
                     const int iu0 = s_tap[rs][0];
                     float2 res = make_float2(0.0f, 0.0f);
                     if (iu0 >= 0)
@@ -1235,7 +1237,7 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
                 const bool ok = v < b;
                 // Column i of T only sees column i of B: a lane past the
                 // window reads a staged row and its result is dropped below.
-                const int rs = (ok ? v : a) % kDftCap;
+                const int rs = (ok ? v : a) & (kDftCap - 1);
                 f32x4 t_re = {0.0f, 0.0f, 0.0f, 0.0f};
                 f32x4 t_im = {0.0f, 0.0f, 0.0f, 0.0f};
                 float2 bv[4];
