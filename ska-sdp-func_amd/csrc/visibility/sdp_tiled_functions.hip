@@ -200,6 +200,18 @@ __global__ void k_tile_write(TileGeom g, const U* __restrict__ uvw,
     if (o.vis_index) o.vis_index[pos] = v;
 }
 
+// Sets *bad when some tile's run [offsets[k], offsets[k] + counts[k]) does
+// not lie inside the caller's sorted arrays [0, cap).
+__global__ void k_check_fit(const int* __restrict__ offsets,
+        const int* __restrict__ counts, int64_t ntiles, int64_t cap,
+        int* __restrict__ bad)
+{
+    const int64_t k = blockIdx.x * (int64_t)kThreads + threadIdx.x;
+    if (k >= ntiles || counts[k] == 0) return;
+    const int64_t lo = offsets[k], hi = lo + counts[k];
+    if (lo < 0 || hi > cap) *bad = 1;
+}
+
 __global__ void k_advance(int* __restrict__ offsets,
         const int* __restrict__ counts, int64_t ntiles)
 {
@@ -331,6 +343,38 @@ void sort_tiles(const TileGeom& g, const U* uvw, const U* freq,
                 tstart, (int)(nt + 1)), status);
         SDP_HIP_CHECK(hipMemcpy(&n_entries, eoff + g.nvis, sizeof(int),
                 hipMemcpyDeviceToHost), status);
+    }
+    // The caller's offsets plus this call's per-tile counts must fit the
+    // sorted arrays: refuse rather than truncate (a truncated write would
+    // leave the advanced cursors inconsistent with what was stored).
+    if (!*status && (int64_t)n_entries > o.cap)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Sorted arrays hold %lld entries, %d needed",
+                (long long)o.cap, n_entries);
+    }
+    if (!*status && n_entries > 0)
+    {
+        int bad = 0;
+        SDP_HIP_CHECK(hipMemset(skipped, 0, sizeof(int)), status);
+        k_check_fit<<<blocks(nt), kThreads>>>(offsets, counts, nt, o.cap,
+                skipped);
+        SDP_HIP_CHECK_LAUNCH(status);
+        SDP_HIP_CHECK(hipMemcpy(&bad, skipped, sizeof(int),
+                hipMemcpyDeviceToHost), status);
+        if (!*status && bad)
+        {
+            *status = SDP_ERR_INVALID_ARGUMENT;
+            SDP_LOG_ERROR("tile_offsets + tile counts run past the sorted "
+                    "arrays (%lld entries)", (long long)o.cap);
+        }
+    }
+    if (*status)
+    {
+        int* bufs[] = {counts, nent, eoff, tstart, skipped};
+        for (int* p : bufs) (void)hipFree(p);
+        (void)hipFree(tmp);
+        return;
     }
     alloc(&keys, n_entries);
     alloc(&vals, n_entries);

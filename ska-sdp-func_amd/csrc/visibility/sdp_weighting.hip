@@ -180,6 +180,13 @@ bool check_args(const sdp_Mem* uvw, const sdp_Mem* freq_hz,
     }
     if (*status) return false;
     const sdp_MemLocation loc = sdp_mem_location(output_weight);
+    // dims[] holds the output's {T, B, C, P}; the kernels index the input
+    // with the same flat offsets, so it must live where the output lives
+    // (the reference's GPU path fetches it with sdp_mem_gpu_buffer_const,
+    // which fails with SDP_ERR_MEM_LOCATION) and have the same shape.
+    sdp_mem_check_location(input_weight, loc, status);
+    sdp_mem_check_shape(input_weight, 4, dims, status);
+    if (*status) return false;
     if (!sdp_mem_is_floating_point(uvw) || sdp_mem_is_complex(uvw))
     {
         *status = SDP_ERR_DATA_TYPE;

@@ -36,8 +36,17 @@ def grid_sharded(gridder, uvw, freq, vis, weight, dirty, dist, mode="image",
     gridded image (accumulated onto its input dirty image); other ranks'
     dirty buffers are scratch. grid_buf: [G, G] complex buffer for
     mode="grid" (allocated by the caller, reused across calls).
+
+    dst is a GLOBAL rank, as in torch.distributed.reduce, also when a
+    group is given (it must then be a member of the group); the
+    comparison below therefore uses this process's global rank.
     """
-    rank = dist.get_rank(group) if group is not None else dist.get_rank()
+    rank = dist.get_rank()
+    if group is not None:
+        members = dist.get_process_group_ranks(group)
+        if dst not in members:
+            raise ValueError(f"dst {dst} is not a member of the group "
+                             f"{members}")
     if mode == "image":
         if rank != dst:
             dirty.zero_()

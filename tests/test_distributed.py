@@ -103,6 +103,61 @@ def test_sharded_gridding_matches_unsharded(tmp_path, mode):
     assert err < 1e-12
 
 
+def _group_worker(rank, world, port, mode, result_path):
+    """World 3, sub-group {1, 2}, dst = global rank 2 (group-local rank 1):
+    the image must land on global rank 2, and rank 0 must not take part."""
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    for p in (here, root, os.path.join(root, "ska-sdp-func_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle import es_oracle
+    from ska_sdp_func.grid_data.distributed import grid_sharded, shard_rows
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    group = dist.new_group([1, 2])
+    n = 48
+    uvw, freq, vis, wt, px = make_case(17, 203, 1, n, dbl=True)
+    dirty_in = np.random.default_rng(6).standard_normal((n, n))
+    geo = es_oracle.geometry_for(uvw, freq, vis, dirty_in, px, 1e-10, False)
+    if rank in (1, 2):
+        lo, hi = shard_rows(len(uvw), rank - 1, 2)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+        dirty = t(dirty_in.copy())
+        G = geo["grid_size"]
+        grid_buf = torch.zeros((G, G), dtype=torch.complex128)
+        grid_sharded(OracleGridder(geo), t(uvw[lo:hi]), t(freq),
+                     t(vis[lo:hi]), t(wt[lo:hi]), dirty, dist, mode=mode,
+                     dst=2, group=group, grid_buf=grid_buf)
+        if rank == 2:
+            ref = es_oracle.grid_uvw_es_fft(geo, uvw, freq, vis, wt,
+                                            dirty_in)
+            np.save(result_path, np.array([rel_l2(dirty.numpy(), ref)]))
+        if rank == 1:
+            try:
+                grid_sharded(OracleGridder(geo), t(uvw[:1]), t(freq),
+                             t(vis[:1]), t(wt[:1]), dirty, dist, mode=mode,
+                             dst=0, group=group, grid_buf=grid_buf)
+                raise AssertionError("dst outside the group accepted")
+            except ValueError:
+                pass
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["image", "grid"])
+def test_sharded_gridding_subgroup_global_dst(tmp_path, mode):
+    path = str(tmp_path / "err.npy")
+    mp.spawn(_group_worker, args=(3, _free_port(), mode, path), nprocs=3,
+             join=True)
+    err = float(np.load(path)[0])
+    assert err < 1e-12
+
+
 def test_shard_rows_cover_exactly():
     from ska_sdp_func.grid_data.distributed import shard_rows
 

@@ -132,3 +132,30 @@ def test_gpu_errors(device):
         count_and_prefix_sum(uvw, freqs, vis, 256, 32, 16, CELL, 4,
                              ctypes.c_int(0), off, off[:-1].copy(),
                              np.zeros(1, np.int32))
+
+
+@pytest.mark.gpu
+def test_gpu_undersized_sorted_arrays_rejected(device):
+    """Sorted arrays shorter than the entries (or caller offsets running past
+    them) give SDP_ERR_INVALID_ARGUMENT and leave the cursors untouched,
+    instead of a truncated sort with advanced cursors."""
+    import torch
+    from ska_sdp_func.utility import CError
+    from ska_sdp_func.visibility import tiled_indexing
+    grid, support, C, tu, tv = 256, 4, 4, 32, 16
+    uvw, freqs, vis, w = make_case(C=C)
+    counts, offsets, skipped, total = to.count_and_prefix_sum(
+        uvw, freqs, C, grid, tu, tv, CELL, support)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    T, B = uvw.shape[:2]
+    for cap, off in ((total - 1, offsets),
+                     (total, offsets + np.int32(1))):
+        d_off = d(off.astype(np.int32))
+        arrs = [torch.zeros((cap,), dtype=torch.float64, device=device)
+                for _ in range(2)]
+        ints = [torch.zeros((cap,), dtype=torch.int32, device=device)
+                for _ in range(2)]
+        with pytest.raises(CError, match="Invalid function argument"):
+            tiled_indexing(d(uvw), d(freqs), grid, tu, tv, CELL, support, C,
+                           B, T, ints[0], arrs[0], arrs[1], ints[1], d_off)
+        np.testing.assert_array_equal(d_off.cpu().numpy(), off)

@@ -116,3 +116,12 @@ def test_gpu_argument_errors(device):
     with pytest.raises(CError, match="Memory location"):
         uniform_weights(uvw, freqs, mx, torch.zeros((3, 3, 1),
                         dtype=torch.float64, device=device), inp, out)
+    # A host input_weight with device outputs is a location error, never a
+    # host pointer handed to a kernel.
+    d = [torch.from_numpy(a).to(device) for a in (uvw, freqs, grid, out)]
+    with pytest.raises(CError, match="Memory location"):
+        uniform_weights(d[0], d[1], mx, d[2], inp, d[3])
+    # An input smaller than the output is rejected, not read past its end.
+    small = torch.from_numpy(np.ascontiguousarray(inp[:, :, :1])).to(device)
+    with pytest.raises(CError):
+        uniform_weights(d[0], d[1], mx, d[2], small, d[3])
