@@ -5,14 +5,18 @@
 // stream sequentially in time with 3-4 qsorts of <= num_channels doubles
 // per step (:125-339). Here one 64-lane wave owns a stream: the channels of
 // a time step live in registers (channel c in lane c % 64, slot c / 64),
-// and every median is an exact order statistic found by a bitwise binary
-// search over the IEEE bit patterns (all the values ranked are >= 0, so
-// bit-pattern order is value order) with one ballot + scalar popcount per
-// register per bit: no sort, no LDS traffic, no barriers. The stream state
-// (previous magnitudes, transit scores) stays in registers across time
-// steps; the median history is a per-wave LDS ring; window flagging reads
-// trigger bytes from LDS. Flags are written only where set (idempotent
-// stores of 1), so the output keeps whatever the caller's array held.
+// and every median is an exact order statistic selected on the IEEE bit
+// patterns (all the values ranked are >= 0, so bit-pattern order is value
+// order). Each statistic is bracketed by its value at the previous time
+// step: one counting pass (compare + ballot + popcount per register) checks
+// that the bracket holds the k-th key and compacts the ~100 keys inside it
+// into LDS, and a bitwise search over those few registers finishes it --
+// no sort. A bracket miss falls back to the search over all keys, so the
+// result never depends on the bracket. The stream state (previous
+// magnitudes, transit scores) stays in registers across time steps; the
+// median history is a per-wave LDS ring; window flagging reads trigger
+// bytes from LDS. Flags are written only where set (idempotent stores of
+// 1), so the output keeps whatever the caller's array held.
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -101,29 +105,257 @@ __device__ __forceinline__ int mid_index(int n)
     return m < n ? m : n - 1;
 }
 
-// k-th smallest (0-based) of the values v[j] with ok[j], over the wave.
-// Bitwise binary search on the bit patterns of non-negative doubles:
-// prefix ends as the largest key with #(key < prefix) <= k, which is the
-// k-th order statistic itself. Bits below low_bit are known to be zero in
-// every candidate (f32-derived magnitudes: 29) and are skipped.
-template<int N>
-__device__ __forceinline__ double select_kth(const double (&v)[N],
-        const bool (&ok)[N], int k, int low_bit)
+// ---------------------------------------------------------------------------
+// Exact order statistics over a wave.
+//
+// Every value ranked is >= 0, so the IEEE bit pattern orders like the value:
+// a statistic is selected on integer keys (float -> 32-bit, double -> 64-bit
+// patterns). Elements that do not take part carry the key ~0 (above every
+// non-negative pattern, NaNs included), so counting needs no masks.
+//
+// search() is a bitwise binary search for the k-th smallest key inside an
+// interval [L, U) known to hold it (c0 = #(key < L) <= k < c1 = #(key < U)).
+// Each probe costs one compare + ballot + popcount per register; probes that
+// fall outside (L, U) are decided without counting, and the search ends as
+// soon as the interval holds a single key, which is then read out directly.
+//
+// select_tracked() brackets each statistic by the previous time step's value
+// (x +- w per statistic and stream): one pass counts the keys below and inside
+// the bracket and compacts the inside ones into LDS; if the k-th key is inside
+// and the bracket holds <= 64 R keys, the search runs on R registers of
+// candidates instead of all of them. A miss falls back to the search over all
+// keys (still exact); w adapts so that the bracket holds ~32 R candidates.
+// Results never depend on the bracket -- only the cost does.
+// ---------------------------------------------------------------------------
+template<typename V> struct KeyOf;
+template<> struct KeyOf<float>
 {
-    uint64_t key[N];
+    using type = uint32_t;
+    static constexpr int kTop = 30;     // highest bit of a non-negative key
+};
+template<> struct KeyOf<double>
+{
+    using type = uint64_t;
+    static constexpr int kTop = 62;
+};
+
+__device__ __forceinline__ uint32_t key_of(float v) { return __float_as_uint(v); }
+__device__ __forceinline__ uint64_t key_of(double v)
+{
+    return (uint64_t)__double_as_longlong(v);
+}
+__device__ __forceinline__ float val_of(uint32_t k) { return __uint_as_float(k); }
+__device__ __forceinline__ double val_of(uint64_t k)
+{
+    return __longlong_as_double((long long)k);
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p)
+{
+    return __builtin_amdgcn_ballot_w64(p);
+}
+
+__device__ __forceinline__ uint32_t readlane(uint32_t v, int lane)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ __forceinline__ uint64_t readlane(uint64_t v, int lane)
+{
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v,
+            lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(
+            (int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// flags[row + (lane + 64 j) P] = 1 as a uniform row base (scalar) plus one
+// 32-bit per-lane offset, so no per-element address stays live.
+__device__ __forceinline__ void set_flag(int32_t* row, int j, int P, int lane)
+{
+    char* base = (char*)(row + 64 * j * P);
+    *(int32_t*)(base + (uint32_t)(lane * P) * 4u) = 1;
+}
+
+__device__ __forceinline__ int lane_prefix(uint64_t mask)
+{
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+template<typename K, int N>
+__device__ __forceinline__ int count_lt(const K (&key)[N], K c)
+{
+    int s = 0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) key[j] = (uint64_t)__double_as_longlong(v[j]);
-    uint64_t prefix = 0;
-    for (int bit = 62; bit >= low_bit; --bit)
+    for (int j = 0; j < N; ++j) s += __popcll(ballot(key[j] < c));
+    return s;
+}
+
+template<typename K, int N>
+__device__ __forceinline__ K search(const K (&key)[N], int k, K prefix,
+        int bit, K L, K U, int c0, int c1)
+{
+    while (c1 - c0 > 1 && bit >= 0)
     {
-        const uint64_t cand = prefix | (1ull << bit);
-        int cnt = 0;
+        const K cand = prefix | ((K)1 << bit);
+        if (cand <= L)
+        {
+            prefix = cand;
+        }
+        else if (cand < U)
+        {
+            const int cnt = count_lt<K, N>(key, cand);
+            if (cnt <= k)
+            {
+                prefix = cand;
+                L = cand;
+                c0 = cnt;
+            }
+            else
+            {
+                U = cand;
+                c1 = cnt;
+            }
+        }
+        --bit;
+    }
+    if (c1 - c0 > 1) return prefix;        // every bit decided: ties
+    K ans = L;                             // the one key in [L, U)
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+    {
+        const uint64_t m = ballot(key[j] >= L && key[j] < U);
+        if (m) ans = readlane(key[j], (int)__builtin_ctzll(m));
+    }
+    return ans;
+}
+
+struct Track
+{
+    double x, w;     // previous value, bracket half-width
+    bool valid;
+};
+
+template<typename V, int N, int R>
+__device__ __forceinline__ V select_tracked(
+        const typename KeyOf<V>::type (&key)[N], int k, int nvalid,
+        Track& tr, typename KeyOf<V>::type* cand_lds, int lane)
+{
+    using K = typename KeyOf<V>::type;
+    constexpr int kTop = KeyOf<V>::kTop;
+    constexpr K kSpan = (K)1 << (kTop + 1);
+    constexpr bool kCompact = N > R;
+    constexpr int kCap = 64 * R;
+    // Search set: all keys, or the compacted bracket candidates.
+    K prefix = 0, L = 0, U = kSpan;
+    int bit = kTop, c0 = 0, c1 = nvalid, kk = k, n_in = 0;
+    bool hit = false, use_cand = false;
+    if (tr.valid)
+    {
+        const V xv = (V)tr.x, wv = (V)tr.w;
+        V lo_v = xv - wv;
+        if (!(lo_v > (V)0)) lo_v = (V)0;
+        K lo = key_of(lo_v), hi = key_of(xv + wv);
+        if (!(hi < kSpan)) hi = kSpan - 1;
+        if (lo > hi) lo = hi;
+        int c_lt = 0;
 #pragma unroll
         for (int j = 0; j < N; ++j)
-            cnt += __popcll(__ballot(ok[j] && key[j] < cand));
-        if (cnt <= k) prefix = cand;
+        {
+            const bool below = key[j] < lo;
+            const bool inside = !below && key[j] <= hi;
+            const uint64_t mb = ballot(below), mi = ballot(inside);
+            if (kCompact)
+            {
+                const int pos = n_in + lane_prefix(mi);
+                if (inside && pos < kCap) cand_lds[pos] = key[j];
+            }
+            c_lt += __popcll(mb);
+            n_in += __popcll(mi);
+        }
+        if (c_lt <= k && k < c_lt + n_in)
+        {
+            hit = true;
+            L = lo;
+            U = hi + 1;
+            c0 = c_lt;
+            c1 = c_lt + n_in;
+            if (lo == hi)
+            {
+                prefix = lo;
+                bit = -1;
+            }
+            else
+            {
+                bit = (int)(8 * sizeof(K)) - 1 -
+                        (sizeof(K) == 8 ? __clzll((long long)(lo ^ hi)) :
+                                          __clz((int)(lo ^ hi)));
+                prefix = lo & ~(((K)2 << bit) - 1);
+            }
+            if (kCompact && n_in <= kCap)
+            {
+                use_cand = true;
+                kk = k - c_lt;
+                c0 = 0;
+                c1 = n_in;
+            }
+        }
+        else if (k < c_lt)
+        {
+            U = lo;
+            c1 = c_lt;
+        }
+        else
+        {
+            L = hi + 1;
+            c0 = c_lt + n_in;
+        }
     }
-    return __longlong_as_double((long long)prefix);
+    K ans;
+    if (kCompact && use_cand)
+    {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        K c[kCompact ? R : 1];
+#pragma unroll
+        for (int r = 0; r < (kCompact ? R : 1); ++r)
+        {
+            const int s = lane + 64 * r;
+            c[r] = s < n_in ? cand_lds[s] : ~(K)0;
+        }
+        ans = search<K, kCompact ? R : 1>(c, kk, prefix, bit, L, U, c0, c1);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    else
+    {
+        ans = search<K, N>(key, kk, prefix, bit, L, U, c0, c1);
+    }
+
+    // Bracket for the next time step: centred on this value, half-width
+    // scaled so the bracket holds about `target` keys.
+    const double a = (double)val_of(ans);
+    const double target = fmin(32.0 * R, fmax(1.0, 0.125 * nvalid));
+    if (!tr.valid)
+    {
+        tr.w = a * 0x1p-7;
+    }
+    else if (hit)
+    {
+        double f = target / (n_in > 1 ? n_in : 1);
+        if (n_in <= kCap) f = f < 0.5 ? 0.5 : (f > 2.0 ? 2.0 : f);
+        tr.w *= f;
+    }
+    else if (!(tr.w > 0.0))
+    {
+        const double d = fabs(a - tr.x);
+        tr.w = (d > 0.0) ? d : a * 0x1p-10;
+    }
+    if (!(tr.w <= fabs(a) * 1024.0)) tr.w = fabs(a) * 1024.0;
+    if (!(tr.w >= 0.0)) tr.w = 0.0;
+    tr.x = a;
+    tr.valid = isfinite(a);
+    return val_of(ans);
 }
 
 // (:104-122)
@@ -134,6 +366,51 @@ __device__ __forceinline__ double modified_zscore(double median,
     if (mediandev == 0 && val == median) return 0.0;
     if (mediandev == 0 && val != median) return 10000000.0;
     return 0.6795 * (val - median) / mediandev;
+}
+
+// modified_zscore compared with a threshold:
+// z > thr || z < -thr  <=>  |z| > thr (for every thr, NaNs included).
+// The division is replaced by a multiply with the reciprocal wherever that
+// cannot change the outcome: |q - z| <= 2^-50 |z| for normal divisors, so
+// only values within 2^-44 thr of the threshold take the exact division.
+struct ZTest
+{
+    double med, dev, inv, thr, band;
+    bool dev0, fast;
+};
+
+__device__ __forceinline__ ZTest make_ztest(double med, double dev,
+        double thr)
+{
+    ZTest z;
+    z.med = med;
+    z.dev = dev;
+    z.thr = thr;
+    z.dev0 = (dev == 0);
+    const double adev = fabs(dev);
+    z.fast = adev > 0x1p-1000 && adev < 0x1p+1000 &&
+            thr > 0x1p-900 && thr < 0x1p+900;
+    z.inv = z.fast ? 1.0 / dev : 0.0;
+    z.band = thr * 0x1p-44;
+    return z;
+}
+
+__device__ __forceinline__ bool z_exceeds(const ZTest& zt, double val)
+{
+#pragma clang fp contract(off)
+    if (zt.dev0)
+    {
+        const double z = (val == zt.med) ? 0.0 : 10000000.0;
+        return z > zt.thr || z < -zt.thr;
+    }
+    const double num = 0.6795 * (val - zt.med);
+    if (zt.fast)
+    {
+        const double aq = fabs(num * zt.inv);
+        if (!(fabs(aq - zt.thr) <= zt.band)) return aq > zt.thr;
+    }
+    const double z = num / zt.dev;
+    return z > zt.thr || z < -zt.thr;
 }
 
 __device__ __forceinline__ void wave_sync()
@@ -157,61 +434,112 @@ __device__ __forceinline__ bool spread(const uint8_t* trig, int d, int C,
     return f;
 }
 
-template<typename FP, int EPL, int HEPL>
-__global__ __launch_bounds__(64 * kWaves) void k_flagger(
+// Tuning hook: e.g. -DFLAGGER_WAVES="__attribute__((amdgpu_waves_per_eu(3)))"
+// (measured: 3 or 4 waves per SIMD by spilling ran 2-6 % slower than the
+// compiler's own allocation at config 5).
+#ifndef FLAGGER_WAVES
+#define FLAGGER_WAVES
+#endif
+constexpr int kCandRegs = 3;      // compacted candidates: 192 per statistic
+
+// Per-wave LDS layout: median history | trigger bytes (all, variation) |
+// candidate keys.
+__host__ __device__ inline size_t lds_per_wave(int wmh, int C)
+{
+    return (size_t)wmh * 8 + 2 * (size_t)((C + 15) & ~15) +
+            64 * kCandRegs * 8;
+}
+
+// FULL: sampling_step 1 and C == 64 EPL, so every register slot is a sampled
+// channel and the magnitude / transit arrays are their own keys.
+template<typename FP, int EPL, int HEPL, bool FULL>
+__global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
         const FP* __restrict__ vis, int32_t* __restrict__ flags,
         FlagParams prm)
 {
 #pragma clang fp contract(off)
+    using KM = typename KeyOf<FP>::type;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane0 = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t stream = (int64_t)blockIdx.x * kWaves + wave;
     if (stream >= prm.B * prm.P) return;   // whole wave
     const int64_t b = stream / prm.P;
     const int p = (int)(stream % prm.P);
-    const int C = prm.C, P = prm.P;
-    // Per-wave LDS: median history ring | trigger bytes (all, variation).
-    const size_t per_wave = (size_t)prm.wmh * 8 + 2 * (size_t)((C + 15) & ~15);
-    unsigned char* base = smem + per_wave * wave;
+    const int C = prm.C;
+    const int cpad = (C + 15) & ~15;
+    unsigned char* base = smem + lds_per_wave(prm.wmh, C) * wave;
     double* hist = (double*)base;
     uint8_t* trig_all = base + (size_t)prm.wmh * 8;
-    uint8_t* trig_var = trig_all + ((C + 15) & ~15);
-    const int low_bit_mag = sizeof(FP) == 4 ? 29 : 0;
+    uint8_t* trig_var = trig_all + cpad;
+    void* cand = trig_var + cpad;
     const int k_s = mid_index(prm.ns);
 
     bool ch_ok[EPL], smp_ok[EPL];
 #pragma unroll
     for (int j = 0; j < EPL; ++j)
     {
-        const int c = lane + 64 * j;
-        ch_ok[j] = c < C;
-        smp_ok[j] = c < C && (c % prm.step) == 0 && (c / prm.step) < prm.ns;
+        const int c = lane0 + 64 * j;
+        ch_ok[j] = FULL || c < C;
+        smp_ok[j] = FULL || (c < C && (c % prm.step) == 0 &&
+                (c / prm.step) < prm.ns);
     }
-    double prev[EPL], transit[EPL];
+    FP m[EPL], prev[EPL];
+    double transit[EPL];
 #pragma unroll
-    for (int j = 0; j < EPL; ++j) prev[j] = transit[j] = 0.0;
+    for (int j = 0; j < EPL; ++j)
+    {
+        prev[j] = (FP)0;
+        transit[j] = 0.0;
+    }
+    Track tk_mag{0, 0, false}, tk_dev{0, 0, false};
+    Track tk_var{0, 0, false}, tk_vdev{0, 0, false};
+    Track tk_h{0, 0, false}, tk_hdev{0, 0, false};
 
-    const int64_t time_block = prm.B * (int64_t)C * P;
+    const int64_t time_block = prm.B * (int64_t)C * prm.P;
     for (int64_t t = 0; t < prm.T; ++t)
     {
+        // Opaque per step, so that the per-element address and LDS offset
+        // arithmetic is not hoisted out of the time loop as dozens of
+        // loop-invariant registers.
+        int P = prm.P, lane = lane0;
+        asm volatile("" : "+s"(P));
+        asm volatile("" : "+v"(lane));
         const int64_t row = t * time_block + b * (int64_t)C * P + p;
-        double m[EPL];
+        // Uniform row bases; per-element offsets are 32-bit (C * P < 2^31).
+        const FP* vrow = vis + 2 * row;
+        int32_t* frow = flags + row;
+        int32_t* fprev = frow - time_block;
 #pragma unroll
         for (int j = 0; j < EPL; ++j)
         {
-            m[j] = 0.0;
+            m[j] = (FP)0;
             if (ch_ok[j])
             {
-                const FP* z = vis + 2 * (row + (int64_t)(lane + 64 * j) * P);
-                m[j] = mag_of(z[0], z[1]);
+                const char* zb = (const char*)(vrow + 128 * j * P);
+                const FP* z = (const FP*)(zb + (uint32_t)(lane * P) *
+                        (2 * sizeof(FP)));
+                m[j] = (FP)mag_of(z[0], z[1]);
             }
         }
         // Magnitude median and MAD over the sampled channels (:170-178).
-        const double median = select_kth<EPL>(m, smp_ok, k_s, low_bit_mag);
-        double dv[EPL];
+        double median, mediandev;
+        {
+            KM km[EPL];
 #pragma unroll
-        for (int j = 0; j < EPL; ++j) dv[j] = fabs(m[j] - median);
-        const double mediandev = select_kth<EPL>(dv, smp_ok, k_s, 0);
+            for (int j = 0; j < EPL; ++j)
+                km[j] = smp_ok[j] ? key_of(m[j]) : ~(KM)0;
+            median = (double)select_tracked<FP, EPL, kCandRegs>(km, k_s,
+                    prm.ns, tk_mag, (KM*)cand, lane);
+        }
+        {
+            uint64_t kd[EPL];
+#pragma unroll
+            for (int j = 0; j < EPL; ++j)
+                kd[j] = smp_ok[j] ? key_of(fabs((double)m[j] - median)) :
+                                    ~(uint64_t)0;
+            mediandev = select_tracked<double, EPL, kCandRegs>(kd, k_s,
+                    prm.ns, tk_dev, (uint64_t*)cand, lane);
+        }
 
         // Broadband: median history of the last min(t + 1, wmh) steps.
         if (lane == 0) hist[t % prm.wmh] = median;
@@ -221,32 +549,42 @@ __global__ __launch_bounds__(64 * kWaves) void k_flagger(
         if (t != 0)
         {
             double hv[HEPL];
-            bool hok[HEPL];
+            uint64_t hk[HEPL];
 #pragma unroll
             for (int j = 0; j < HEPL; ++j)
             {
                 const int tt = lane + 64 * j;
-                hok[j] = tt < medwindow;
-                hv[j] = hok[j] ? hist[(t - tt) % prm.wmh] : 0.0;
+                const bool ok = tt < medwindow;
+                hv[j] = ok ? hist[(t - tt) % prm.wmh] : 0.0;
+                hk[j] = ok ? key_of(hv[j]) : ~(uint64_t)0;
             }
             const int k_h = mid_index(medwindow);
-            const double medmed = select_kth<HEPL>(hv, hok, k_h, 0);
+            const double medmed = select_tracked<double, HEPL, kCandRegs>(
+                    hk, k_h, medwindow, tk_h, (uint64_t*)cand, lane);
 #pragma unroll
-            for (int j = 0; j < HEPL; ++j) hv[j] = fabs(hv[j] - medmed);
-            const double medmeddev = select_kth<HEPL>(hv, hok, k_h, 0);
+            for (int j = 0; j < HEPL; ++j)
+            {
+                if (hk[j] != ~(uint64_t)0) hk[j] = key_of(fabs(hv[j] - medmed));
+            }
+            const double medmeddev = select_tracked<double, HEPL, kCandRegs>(
+                    hk, k_h, medwindow, tk_hdev, (uint64_t*)cand, lane);
             const double zmed = modified_zscore(medmed, medmeddev, median);
             situation = zmed > prm.thr_bb || zmed < -prm.thr_bb;
         }
 
-        // Magnitude triggers (:214-241).
-        bool trig[EPL], tv[EPL];
-#pragma unroll
-        for (int j = 0; j < EPL; ++j)
+        // Magnitude triggers (:214-241) into trig_all.
         {
-            const double z = modified_zscore(median, mediandev, m[j]);
-            trig[j] = ch_ok[j] &&
-                    (z > prm.thr_mag || z < -prm.thr_mag || situation);
-            tv[j] = false;
+            const ZTest zt = make_ztest(median, mediandev, prm.thr_mag);
+#pragma unroll
+            for (int j = 0; j < EPL; ++j)
+            {
+                const bool tr = ch_ok[j] &&
+                        (situation || z_exceeds(zt, (double)m[j]));
+                const int c = lane + 64 * j;
+                if (prm.window > 0 && ch_ok[j]) trig_all[c] = tr ? 1 : 0;
+                if (prm.window == 0 && tr)
+                    set_flag(frow, j, P, lane);
+            }
         }
 
         // Fluctuations (:245-339).
@@ -255,93 +593,120 @@ __global__ __launch_bounds__(64 * kWaves) void k_flagger(
 #pragma unroll
             for (int j = 0; j < EPL; ++j)
             {
-                const double rate = fabs(prev[j] - m[j]);
+                const double rate = fabs((double)prev[j] - (double)m[j]);
                 transit[j] = (t == 1) ? rate :
                         prm.alpha * rate + (1 - prm.alpha) * transit[j];
             }
-            const double medianvar = select_kth<EPL>(transit, smp_ok, k_s, 0);
-            // MAD around the MAGNITUDE median (:292-295).
+            double medianvar, mediandevvar;
+            {
+                uint64_t kt[EPL];
 #pragma unroll
-            for (int j = 0; j < EPL; ++j) dv[j] = fabs(transit[j] - median);
-            const double mediandevvar = select_kth<EPL>(dv, smp_ok, k_s, 0);
+                for (int j = 0; j < EPL; ++j)
+                    kt[j] = smp_ok[j] ? key_of(transit[j]) : ~(uint64_t)0;
+                medianvar = select_tracked<double, EPL, kCandRegs>(kt, k_s,
+                        prm.ns, tk_var, (uint64_t*)cand, lane);
+            }
+            {
+                // MAD around the MAGNITUDE median (:292-295).
+                uint64_t kv[EPL];
+#pragma unroll
+                for (int j = 0; j < EPL; ++j)
+                    kv[j] = smp_ok[j] ? key_of(fabs(transit[j] - median)) :
+                                        ~(uint64_t)0;
+                mediandevvar = select_tracked<double, EPL, kCandRegs>(kv,
+                        k_s, prm.ns, tk_vdev, (uint64_t*)cand, lane);
+            }
+            const ZTest zv = make_ztest(medianvar, mediandevvar, prm.thr_var);
 #pragma unroll
             for (int j = 0; j < EPL; ++j)
             {
-                const double z = modified_zscore(medianvar, mediandevvar,
-                        fabs(transit[j]));
-                tv[j] = ch_ok[j] && (z > prm.thr_var || z < -prm.thr_var);
+                const bool tv = ch_ok[j] && z_exceeds(zv, fabs(transit[j]));
+                const int c = lane + 64 * j;
+                if (prm.window > 0)
+                {
+                    if (ch_ok[j])
+                    {
+                        trig_var[c] = tv ? 1 : 0;
+                        if (tv) trig_all[c] = 1;
+                    }
+                }
+                else if (tv)
+                {
+                    set_flag(frow, j, P, lane);
+                    set_flag(fprev, j, P, lane);
+                }
             }
         }
 
         // Window spread and flag stores: row t gets magnitude | variation
         // triggers, row t - 1 the variation triggers again (:311-338).
-#pragma unroll
-        for (int j = 0; j < EPL; ++j)
+        if (prm.window > 0)
         {
-            const int c = lane + 64 * j;
-            if (c < C)
+            wave_sync();
+#pragma unroll 1
+            for (int j = 0; j < EPL; ++j)
             {
-                trig_all[c] = (trig[j] || tv[j]) ? 1 : 0;
-                trig_var[c] = tv[j] ? 1 : 0;
+                const int c = lane + 64 * j;
+                if (!ch_ok[j]) continue;
+                if (spread(trig_all, c, C, prm.window))
+                    set_flag(frow, j, P, lane);
+                if (t > 0 && spread(trig_var, c, C, prm.window))
+                    set_flag(fprev, j, P, lane);
             }
+            wave_sync();
         }
-        wave_sync();
-#pragma unroll
-        for (int j = 0; j < EPL; ++j)
-        {
-            const int c = lane + 64 * j;
-            if (c >= C) continue;
-            if (spread(trig_all, c, C, prm.window))
-                flags[row + (int64_t)c * P] = 1;
-            if (t > 0 && spread(trig_var, c, C, prm.window))
-                flags[row - time_block + (int64_t)c * P] = 1;
-        }
-        wave_sync();
 #pragma unroll
         for (int j = 0; j < EPL; ++j) prev[j] = m[j];
     }
 }
 
-template<typename FP, int EPL>
+template<typename FP, int EPL, bool FULL>
 sdp_Error launch_epl(const FP* vis, int32_t* flags, const FlagParams& prm)
 {
     sdp_Error st = SDP_SUCCESS;
     const int64_t streams = prm.B * prm.P;
     const unsigned blocks = (unsigned)((streams + kWaves - 1) / kWaves);
-    const size_t lds = kWaves * ((size_t)prm.wmh * 8 +
-            2 * (size_t)((prm.C + 15) & ~15));
+    const size_t lds = kWaves * lds_per_wave(prm.wmh, prm.C);
+    auto run = [&](auto kern) {
+        if (lds > 64 * 1024)
+            SDP_HIP_CHECK(hipFuncSetAttribute((const void*)kern,
+                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                    &st);
+        kern<<<blocks, 64 * kWaves, lds, 0>>>(vis, flags, prm);
+    };
     if (prm.wmh <= 64)
-    {
-        if (lds > 64 * 1024)
-            SDP_HIP_CHECK(hipFuncSetAttribute(
-                    (const void*)k_flagger<FP, EPL, 1>,
-                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), &st);
-        k_flagger<FP, EPL, 1><<<blocks, 64 * kWaves, lds, 0>>>(vis, flags,
-                prm);
-    }
+        run(k_flagger<FP, EPL, 1, FULL>);
+#ifndef SDP_FLAGGER_DEV
     else
-    {
-        if (lds > 64 * 1024)
-            SDP_HIP_CHECK(hipFuncSetAttribute(
-                    (const void*)k_flagger<FP, EPL, 16>,
-                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds), &st);
-        k_flagger<FP, EPL, 16><<<blocks, 64 * kWaves, lds, 0>>>(vis, flags,
-                prm);
-    }
+        run(k_flagger<FP, EPL, 16, FULL>);
+#endif
     SDP_HIP_CHECK_LAUNCH(&st);
     return st;
+}
+
+template<typename FP, int EPL>
+sdp_Error launch_full(const FP* vis, int32_t* flags, const FlagParams& prm)
+{
+    if (prm.step == 1 && prm.C == 64 * EPL)
+        return launch_epl<FP, EPL, true>(vis, flags, prm);
+    return launch_epl<FP, EPL, false>(vis, flags, prm);
 }
 
 template<typename FP>
 sdp_Error launch(const FP* vis, int32_t* flags, const FlagParams& prm)
 {
+#ifdef SDP_FLAGGER_DEV   // register-pressure experiments: one kernel only
+    if (sizeof(FP) == 4) return launch_epl<FP, 16, true>(vis, flags, prm);
+    return SDP_ERR_RUNTIME;
+#else
     const int epl = (prm.C + 63) / 64;
-    if (epl <= 1) return launch_epl<FP, 1>(vis, flags, prm);
-    if (epl <= 2) return launch_epl<FP, 2>(vis, flags, prm);
-    if (epl <= 4) return launch_epl<FP, 4>(vis, flags, prm);
-    if (epl <= 8) return launch_epl<FP, 8>(vis, flags, prm);
-    if (epl <= 16) return launch_epl<FP, 16>(vis, flags, prm);
-    return launch_epl<FP, 32>(vis, flags, prm);
+    if (epl <= 1) return launch_full<FP, 1>(vis, flags, prm);
+    if (epl <= 2) return launch_full<FP, 2>(vis, flags, prm);
+    if (epl <= 4) return launch_full<FP, 4>(vis, flags, prm);
+    if (epl <= 8) return launch_full<FP, 8>(vis, flags, prm);
+    if (epl <= 16) return launch_full<FP, 16>(vis, flags, prm);
+    return launch_full<FP, 32>(vis, flags, prm);
+#endif
 }
 
 // Argument checks of the reference (check_params_dynamic,
