@@ -18,6 +18,7 @@
 // bytes from LDS. Flags are written only where set (idempotent stores of
 // 1), so the output keeps whatever the caller's array held.
 #include <cmath>
+#include <cstdio>
 #include <cstdint>
 #include <cstring>
 
@@ -193,7 +194,7 @@ __device__ __forceinline__ int count_lt(const K (&key)[N], K c)
 
 template<typename K, int N>
 __device__ __forceinline__ K search(const K (&key)[N], int k, K prefix,
-        int bit, K L, K U, int c0, int c1)
+        int bit, K L, K U, int c0, int c1, int& nprobe)
 {
     while (c1 - c0 > 1 && bit >= 0)
     {
@@ -205,6 +206,7 @@ __device__ __forceinline__ K search(const K (&key)[N], int k, K prefix,
         else if (cand < U)
         {
             const int cnt = count_lt<K, N>(key, cand);
+            ++nprobe;
             if (cnt <= k)
             {
                 prefix = cand;
@@ -230,6 +232,12 @@ __device__ __forceinline__ K search(const K (&key)[N], int k, K prefix,
     return ans;
 }
 
+#ifdef SDP_FLAGGER_STATS
+// Per statistic: [init, hit (compacted), hit (all keys), miss, probes over
+// candidates, probes over all keys, hit at the second bracket].
+__device__ unsigned long long g_flag_stats[6][7];
+#endif
+
 struct Track
 {
     double x, w;     // previous value, bracket half-width
@@ -239,7 +247,7 @@ struct Track
 template<typename V, int N, int R>
 __device__ __forceinline__ V select_tracked(
         const typename KeyOf<V>::type (&key)[N], int k, int nvalid,
-        Track& tr, typename KeyOf<V>::type* cand_lds, int lane)
+        Track& tr, typename KeyOf<V>::type* cand_lds, int lane, int sid)
 {
     using K = typename KeyOf<V>::type;
     constexpr int kTop = KeyOf<V>::kTop;
@@ -248,69 +256,85 @@ __device__ __forceinline__ V select_tracked(
     constexpr int kCap = 64 * R;
     // Search set: all keys, or the compacted bracket candidates.
     K prefix = 0, L = 0, U = kSpan;
-    int bit = kTop, c0 = 0, c1 = nvalid, kk = k, n_in = 0;
+    int bit = kTop, c0 = 0, c1 = nvalid, kk = k, n_in = 0, attempt = 0;
     bool hit = false, use_cand = false;
     if (tr.valid)
     {
-        const V xv = (V)tr.x, wv = (V)tr.w;
-        V lo_v = xv - wv;
-        if (!(lo_v > (V)0)) lo_v = (V)0;
-        K lo = key_of(lo_v), hi = key_of(xv + wv);
-        if (!(hi < kSpan)) hi = kSpan - 1;
-        if (lo > hi) lo = hi;
-        int c_lt = 0;
+        // Attempt 0: the bracket x +- w. On a miss, attempt 1 looks 4 w
+        // further on the side of the miss before falling back to the search
+        // over every key (which starts from the interval the misses left).
+        double lo_d = tr.x - tr.w, hi_d = tr.x + tr.w;
+#pragma unroll 1
+        for (; attempt < 2; ++attempt)
+        {
+            V lo_v = (V)lo_d;
+            if (!(lo_v > (V)0)) lo_v = (V)0;
+            K lo = key_of(lo_v), hi = key_of((V)hi_d);
+            if (!(hi < kSpan)) hi = kSpan - 1;
+            if (lo < L) lo = L;
+            if (hi > U - 1) hi = U - 1;
+            if (lo > hi) break;
+            int c_lt = 0;
+            n_in = 0;
 #pragma unroll
-        for (int j = 0; j < N; ++j)
-        {
-            const bool below = key[j] < lo;
-            const bool inside = !below && key[j] <= hi;
-            const uint64_t mb = ballot(below), mi = ballot(inside);
-            if (kCompact)
+            for (int j = 0; j < N; ++j)
             {
-                const int pos = n_in + lane_prefix(mi);
-                if (inside && pos < kCap) cand_lds[pos] = key[j];
+                const bool below = key[j] < lo;
+                const bool inside = !below && key[j] <= hi;
+                const uint64_t mb = ballot(below), mi = ballot(inside);
+                if (kCompact)
+                {
+                    const int pos = n_in + lane_prefix(mi);
+                    if (inside && pos < kCap) cand_lds[pos] = key[j];
+                }
+                c_lt += __popcll(mb);
+                n_in += __popcll(mi);
             }
-            c_lt += __popcll(mb);
-            n_in += __popcll(mi);
-        }
-        if (c_lt <= k && k < c_lt + n_in)
-        {
-            hit = true;
-            L = lo;
-            U = hi + 1;
-            c0 = c_lt;
-            c1 = c_lt + n_in;
-            if (lo == hi)
+            if (c_lt <= k && k < c_lt + n_in)
             {
-                prefix = lo;
-                bit = -1;
+                hit = true;
+                L = lo;
+                U = hi + 1;
+                c0 = c_lt;
+                c1 = c_lt + n_in;
+                if (lo == hi)
+                {
+                    prefix = lo;
+                    bit = -1;
+                }
+                else
+                {
+                    bit = (int)(8 * sizeof(K)) - 1 -
+                            (sizeof(K) == 8 ? __clzll((long long)(lo ^ hi)) :
+                                              __clz((int)(lo ^ hi)));
+                    prefix = lo & ~(((K)2 << bit) - 1);
+                }
+                if (kCompact && n_in <= kCap)
+                {
+                    use_cand = true;
+                    kk = k - c_lt;
+                    c0 = 0;
+                    c1 = n_in;
+                }
+                break;
+            }
+            if (k < c_lt)
+            {
+                U = lo;
+                c1 = c_lt;
+                hi_d = lo_d;
+                lo_d = lo_d - 4.0 * tr.w;
             }
             else
             {
-                bit = (int)(8 * sizeof(K)) - 1 -
-                        (sizeof(K) == 8 ? __clzll((long long)(lo ^ hi)) :
-                                          __clz((int)(lo ^ hi)));
-                prefix = lo & ~(((K)2 << bit) - 1);
+                L = hi + 1;
+                c0 = c_lt + n_in;
+                lo_d = hi_d;
+                hi_d = hi_d + 4.0 * tr.w;
             }
-            if (kCompact && n_in <= kCap)
-            {
-                use_cand = true;
-                kk = k - c_lt;
-                c0 = 0;
-                c1 = n_in;
-            }
-        }
-        else if (k < c_lt)
-        {
-            U = lo;
-            c1 = c_lt;
-        }
-        else
-        {
-            L = hi + 1;
-            c0 = c_lt + n_in;
         }
     }
+    int nprobe = 0;
     K ans;
     if (kCompact && use_cand)
     {
@@ -323,28 +347,44 @@ __device__ __forceinline__ V select_tracked(
             const int s = lane + 64 * r;
             c[r] = s < n_in ? cand_lds[s] : ~(K)0;
         }
-        ans = search<K, kCompact ? R : 1>(c, kk, prefix, bit, L, U, c0, c1);
+        ans = search<K, kCompact ? R : 1>(c, kk, prefix, bit, L, U, c0, c1, nprobe);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
     else
     {
-        ans = search<K, N>(key, kk, prefix, bit, L, U, c0, c1);
+        ans = search<K, N>(key, kk, prefix, bit, L, U, c0, c1, nprobe);
     }
 
     // Bracket for the next time step: centred on this value, half-width
     // scaled so the bracket holds about `target` keys.
+#ifdef SDP_FLAGGER_STATS
+    if (lane == 0)
+    {
+        const int cls = !tr.valid ? 0 : (!hit ? 3 : (attempt > 0 ? 6 :
+                (use_cand ? 1 : 2)));
+        atomicAdd(&g_flag_stats[sid][cls], 1ull);
+        atomicAdd(&g_flag_stats[sid][use_cand ? 4 : 5],
+                (unsigned long long)nprobe);
+    }
+#endif
     const double a = (double)val_of(ans);
     const double target = fmin(32.0 * R, fmax(1.0, 0.125 * nvalid));
     if (!tr.valid)
     {
         tr.w = a * 0x1p-7;
     }
-    else if (hit)
+    else if (hit && attempt == 0)
     {
         double f = target / (n_in > 1 ? n_in : 1);
         if (n_in <= kCap) f = f < 0.5 ? 0.5 : (f > 2.0 ? 2.0 : f);
         tr.w *= f;
+    }
+    else if (hit)
+    {
+        // Found one step beyond the bracket (a 4 w wide window): widen.
+        double f = 2.0 * target / (n_in > 1 ? n_in : 1);
+        tr.w *= f < 1.0 ? 1.0 : (f > 2.0 ? 2.0 : f);
     }
     else if (!(tr.w > 0.0))
     {
@@ -496,6 +536,26 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
     Track tk_h{0, 0, false}, tk_hdev{0, 0, false};
 
     const int64_t time_block = prm.B * (int64_t)C * prm.P;
+    const int64_t stream_off = b * (int64_t)C * prm.P + p;
+    // Visibilities of the next time step are loaded while the current one
+    // is processed (one complex value per register slot).
+    typedef FP FP2 __attribute__((ext_vector_type(2)));
+    FP2 raw[EPL];
+    auto load_step = [&](int64_t tt, int P, int lane) {
+        const FP* vrow = vis + 2 * (tt * time_block + stream_off);
+#pragma unroll
+        for (int j = 0; j < EPL; ++j)
+        {
+            if (ch_ok[j])
+            {
+                const char* zb = (const char*)(vrow + 128 * j * P);
+                raw[j] = *(const FP2*)(zb + (uint32_t)(lane * P) *
+                        (2 * sizeof(FP)));
+            }
+        }
+    };
+    load_step(0, prm.P, lane0);
+    double prev_median = 0.0;
     for (int64_t t = 0; t < prm.T; ++t)
     {
         // Opaque per step, so that the per-element address and LDS offset
@@ -504,23 +564,14 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
         int P = prm.P, lane = lane0;
         asm volatile("" : "+s"(P));
         asm volatile("" : "+v"(lane));
-        const int64_t row = t * time_block + b * (int64_t)C * P + p;
-        // Uniform row bases; per-element offsets are 32-bit (C * P < 2^31).
-        const FP* vrow = vis + 2 * row;
+        const int64_t row = t * time_block + stream_off;
         int32_t* frow = flags + row;
         int32_t* fprev = frow - time_block;
 #pragma unroll
         for (int j = 0; j < EPL; ++j)
-        {
-            m[j] = (FP)0;
-            if (ch_ok[j])
-            {
-                const char* zb = (const char*)(vrow + 128 * j * P);
-                const FP* z = (const FP*)(zb + (uint32_t)(lane * P) *
-                        (2 * sizeof(FP)));
-                m[j] = (FP)mag_of(z[0], z[1]);
-            }
-        }
+            m[j] = ch_ok[j] ? (FP)mag_of(raw[j].x, raw[j].y) : (FP)0;
+        if (t + 1 < prm.T) load_step(t + 1, P, lane);
+
         // Magnitude median and MAD over the sampled channels (:170-178).
         double median, mediandev;
         {
@@ -529,7 +580,7 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
             for (int j = 0; j < EPL; ++j)
                 km[j] = smp_ok[j] ? key_of(m[j]) : ~(KM)0;
             median = (double)select_tracked<FP, EPL, kCandRegs>(km, k_s,
-                    prm.ns, tk_mag, (KM*)cand, lane);
+                    prm.ns, tk_mag, (KM*)cand, lane, 0);
         }
         {
             uint64_t kd[EPL];
@@ -538,7 +589,7 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
                 kd[j] = smp_ok[j] ? key_of(fabs((double)m[j] - median)) :
                                     ~(uint64_t)0;
             mediandev = select_tracked<double, EPL, kCandRegs>(kd, k_s,
-                    prm.ns, tk_dev, (uint64_t*)cand, lane);
+                    prm.ns, tk_dev, (uint64_t*)cand, lane, 1);
         }
 
         // Broadband: median history of the last min(t + 1, wmh) steps.
@@ -560,14 +611,14 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
             }
             const int k_h = mid_index(medwindow);
             const double medmed = select_tracked<double, HEPL, kCandRegs>(
-                    hk, k_h, medwindow, tk_h, (uint64_t*)cand, lane);
+                    hk, k_h, medwindow, tk_h, (uint64_t*)cand, lane, 2);
 #pragma unroll
             for (int j = 0; j < HEPL; ++j)
             {
                 if (hk[j] != ~(uint64_t)0) hk[j] = key_of(fabs(hv[j] - medmed));
             }
             const double medmeddev = select_tracked<double, HEPL, kCandRegs>(
-                    hk, k_h, medwindow, tk_hdev, (uint64_t*)cand, lane);
+                    hk, k_h, medwindow, tk_hdev, (uint64_t*)cand, lane, 3);
             const double zmed = modified_zscore(medmed, medmeddev, median);
             situation = zmed > prm.thr_bb || zmed < -prm.thr_bb;
         }
@@ -604,7 +655,7 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
                 for (int j = 0; j < EPL; ++j)
                     kt[j] = smp_ok[j] ? key_of(transit[j]) : ~(uint64_t)0;
                 medianvar = select_tracked<double, EPL, kCandRegs>(kt, k_s,
-                        prm.ns, tk_var, (uint64_t*)cand, lane);
+                        prm.ns, tk_var, (uint64_t*)cand, lane, 4);
             }
             {
                 // MAD around the MAGNITUDE median (:292-295).
@@ -613,8 +664,11 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
                 for (int j = 0; j < EPL; ++j)
                     kv[j] = smp_ok[j] ? key_of(fabs(transit[j] - median)) :
                                         ~(uint64_t)0;
+                // |transit - median| sits about `median` above zero: move
+                // its bracket with the magnitude median.
+                if (tk_vdev.valid) tk_vdev.x += median - prev_median;
                 mediandevvar = select_tracked<double, EPL, kCandRegs>(kv,
-                        k_s, prm.ns, tk_vdev, (uint64_t*)cand, lane);
+                        k_s, prm.ns, tk_vdev, (uint64_t*)cand, lane, 5);
             }
             const ZTest zv = make_ztest(medianvar, mediandevvar, prm.thr_var);
 #pragma unroll
@@ -657,6 +711,7 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
         }
 #pragma unroll
         for (int j = 0; j < EPL; ++j) prev[j] = m[j];
+        prev_median = median;
     }
 }
 
@@ -851,6 +906,18 @@ void sdp_flagger_dynamic_threshold(
                 launch<float>((const float*)d_vis, f, prm) :
                 launch<double>((const double*)d_vis, f, prm);
         if (e) *status = e;
+#ifdef SDP_FLAGGER_STATS
+        unsigned long long st[6][7];
+        (void)hipDeviceSynchronize();
+        (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_flag_stats), sizeof(st));
+        for (int i = 0; i < 6; ++i)
+            fprintf(stderr, "flagger stat %d: init %llu hit_cand %llu "
+                    "hit_all %llu miss %llu probes_cand %llu probes_all %llu "
+                    "hit_second %llu\n", i, st[i][0], st[i][1], st[i][2],
+                    st[i][3], st[i][4], st[i][5], st[i][6]);
+        memset(st, 0, sizeof(st));
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_flag_stats), st, sizeof(st));
+#endif
     }
     if (on_host)
     {
