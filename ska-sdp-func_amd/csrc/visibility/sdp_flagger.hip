@@ -192,41 +192,50 @@ __device__ __forceinline__ int count_lt(const K (&key)[N], K c)
     return s;
 }
 
-template<typename K, int N>
+// CHECKS: decide probes outside (L, U) without counting (worth it over all
+// keys). Without it L and U are implied by prefix and bit, which holds
+// when the set lies inside [prefix, prefix + 2^(bit+1)) -- true of the
+// compacted bracket candidates -- and a probe is one counting pass.
+template<typename K, int N, bool CHECKS>
 __device__ __forceinline__ K search(const K (&key)[N], int k, K prefix,
         int bit, K L, K U, int c0, int c1, int& nprobe)
 {
     while (c1 - c0 > 1 && bit >= 0)
     {
         const K cand = prefix | ((K)1 << bit);
-        if (cand <= L)
+        if (CHECKS && cand <= L)
         {
             prefix = cand;
         }
-        else if (cand < U)
+        else if (!CHECKS || cand < U)
         {
             const int cnt = count_lt<K, N>(key, cand);
             ++nprobe;
             if (cnt <= k)
             {
                 prefix = cand;
-                L = cand;
+                if (CHECKS) L = cand;
                 c0 = cnt;
             }
             else
             {
-                U = cand;
+                if (CHECKS) U = cand;
                 c1 = cnt;
             }
         }
         --bit;
     }
     if (c1 - c0 > 1) return prefix;        // every bit decided: ties
+    if (!CHECKS)
+    {
+        L = prefix;
+        U = prefix + (bit >= 0 ? (K)2 << bit : (K)1);
+    }
     K ans = L;                             // the one key in [L, U)
 #pragma unroll
     for (int j = 0; j < N; ++j)
     {
-        const uint64_t m = ballot(key[j] >= L && key[j] < U);
+        const uint64_t m = ballot(key[j] >= L) & ballot(key[j] < U);
         if (m) ans = readlane(key[j], (int)__builtin_ctzll(m));
     }
     return ans;
@@ -274,18 +283,24 @@ __device__ __forceinline__ V select_tracked(
             if (lo < L) lo = L;
             if (hi > U - 1) hi = U - 1;
             if (lo > hi) break;
+            // One pass: count the keys below the bracket and compact the
+            // ones inside it (positions past the capacity all land on the
+            // spare slot kCap, so the store needs no branch).
             int c_lt = 0;
             n_in = 0;
 #pragma unroll
             for (int j = 0; j < N; ++j)
             {
-                const bool below = key[j] < lo;
-                const bool inside = !below && key[j] <= hi;
-                const uint64_t mb = ballot(below), mi = ballot(inside);
+                const uint64_t mb = ballot(key[j] < lo);
+                const uint64_t mi = ballot(key[j] <= hi) & ~mb;
                 if (kCompact)
                 {
-                    const int pos = n_in + lane_prefix(mi);
-                    if (inside && pos < kCap) cand_lds[pos] = key[j];
+                    const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
+                            (uint32_t)(mi >> 32), __builtin_amdgcn_mbcnt_lo(
+                            (uint32_t)mi, (uint32_t)n_in));
+                    const bool inside = __builtin_amdgcn_inverse_ballot_w64(mi);
+                    cand_lds[inside && pos < (uint32_t)kCap ? pos : kCap] =
+                            key[j];
                 }
                 c_lt += __popcll(mb);
                 n_in += __popcll(mi);
@@ -347,13 +362,14 @@ __device__ __forceinline__ V select_tracked(
             const int s = lane + 64 * r;
             c[r] = s < n_in ? cand_lds[s] : ~(K)0;
         }
-        ans = search<K, kCompact ? R : 1>(c, kk, prefix, bit, L, U, c0, c1, nprobe);
+        ans = search<K, kCompact ? R : 1, false>(c, kk, prefix, bit, L, U,
+                c0, c1, nprobe);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
     else
     {
-        ans = search<K, N>(key, kk, prefix, bit, L, U, c0, c1, nprobe);
+        ans = search<K, N, true>(key, kk, prefix, bit, L, U, c0, c1, nprobe);
     }
 
     // Bracket for the next time step: centred on this value, half-width
@@ -487,7 +503,7 @@ constexpr int kCandRegs = 3;      // compacted candidates: 192 per statistic
 __host__ __device__ inline size_t lds_per_wave(int wmh, int C)
 {
     return (size_t)wmh * 8 + 2 * (size_t)((C + 15) & ~15) +
-            64 * kCandRegs * 8;
+            (64 * kCandRegs + 2) * 8;
 }
 
 // FULL: sampling_step 1 and C == 64 EPL, so every register slot is a sampled
