@@ -22,6 +22,8 @@
 namespace sdp_es {
 
 constexpr int kTile = 64;              // grid tile edge (cells)
+constexpr int kCoarse = 4;             // tiles per bin-numbering block edge
+constexpr int kCoarseTile = kTile * kCoarse;   // 256 cells
 constexpr int kBinsPerPass = 16384;    // LDS histogram capacity (64 KiB)
 constexpr int kPiece = 4096;           // max entries per scatter work item
 constexpr int kMaxChunks = 1024;       // chunks of visibilities per bucketing
@@ -36,8 +38,12 @@ struct EsParams
     int support;        // W
     int do_w;           // w-stacking (3-D) path
     int plane;          // w-plane index processed (3-D), 0 in 2-D
-    int ntiles;         // tiles per axis = ceil(G / kTile)
-    int nbins;          // ntiles^2
+    int ntiles;         // fine tiles per axis = ceil(G / kTile)
+    int ncoarse;        // 4 x 4-tile blocks per axis = ceil(G / kCoarseTile)
+    int ncbins;         // ncoarse^2
+    int nbins;          // tile bins, block-major: 16 per 4 x 4-tile block
+                        // (bin b: block b / 16, tile (b % 16) / 4, b % 4),
+                        // so consecutive work items touch adjacent tiles
     T beta;             // full beta (table value * W)
     T uv_scale;         // G * pixel_size
     T w_scale;

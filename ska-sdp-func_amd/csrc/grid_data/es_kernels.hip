@@ -144,6 +144,31 @@ __device__ __forceinline__ uint64_t bits_idx(double x)
     return (uint64_t)__double_as_longlong(x);
 }
 
+// Bin b -> origin (row, col) of its 64 x 64 tile. Bins are numbered
+// block-major: 16 per 4 x 4-tile block, row-major inside it, so the tile
+// kernels' consecutive work items write / read adjacent tiles (measured
+// 5 % faster tile kernels than row-major bins at config 2).
+template<typename T>
+__device__ __forceinline__ void tile_origin(const EsParams<T>& p, int b,
+        int& r0, int& c0)
+{
+    const int cb = b >> 4, q = b & 15;
+    r0 = ((cb / p.ncoarse) * kCoarse + (q >> 2)) * kTile;
+    c0 = ((cb % p.ncoarse) * kCoarse + (q & 3)) * kTile;
+}
+
+// Bin of the fine tile (tu, tv) in that numbering.
+static_assert(kCoarse == 4, "fine_bin assumes 4 x 4-tile blocks");
+template<typename T>
+__device__ __forceinline__ int fine_bin(const EsParams<T>& p, int tu, int tv)
+{
+    // tu, tv >= 0 (tile indices of in-grid taps): unsigned shifts / masks.
+    const unsigned u = (unsigned)tu, v = (unsigned)tv;
+    return (int)((((u >> 2) * (unsigned)p.ncoarse + (v >> 2)) << 4) |
+            ((u & 3u) << 2) | (v & 3u));
+}
+
+
 // Bucketing kernels ---------------------------------------------------------
 
 template<typename T, int MODE, int NT>
@@ -175,14 +200,14 @@ __global__ __launch_bounds__(NT) void k_bucket_count(EsParams<T> p,
                 for (int tu = tu0; tu <= tu1; ++tu)
                     for (int tv = tv0; tv <= tv1; ++tv)
                     {
-                        const int b = tu * p.ntiles + tv - pass_base;
+                        const int b = fine_bin(p, tu, tv) - pass_base;
                         if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
                     }
             }
             else
             {
-                const int b = ((f.u0 + half) / kTile) * p.ntiles +
-                        (f.v0 + half) / kTile - pass_base;
+                const int b = fine_bin(p, (f.u0 + half) / kTile,
+                        (f.v0 + half) / kTile) - pass_base;
                 if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
             }
         }
@@ -413,7 +438,7 @@ __global__ __launch_bounds__(NT) void k_bucket_fill(EsParams<T> p,
                 for (int tu = tu0; tu <= tu1; ++tu)
                     for (int tv = tv0; tv <= tv1; ++tv)
                     {
-                        const int b = tu * p.ntiles + tv - pass_base;
+                        const int b = fine_bin(p, tu, tv) - pass_base;
                         if (b < 0 || b >= nb) continue;
                         const uint32_t pos = atomicAdd(&cursor[b], 1u);
                         store_rec<T, kWords>(recs + (size_t)pos * kWords, rec);
@@ -423,8 +448,8 @@ __global__ __launch_bounds__(NT) void k_bucket_fill(EsParams<T> p,
             {
                 rec[2] = copysign(f.kw, f.flip);
                 rec[3] = idx_bits(T(0), (uint64_t)i);
-                const int b = ((f.u0 + half) / kTile) * p.ntiles +
-                        (f.v0 + half) / kTile - pass_base;
+                const int b = fine_bin(p, (f.u0 + half) / kTile,
+                        (f.v0 + half) / kTile) - pass_base;
                 if (b < 0 || b >= nb) continue;
                 const uint32_t pos = atomicAdd(&cursor[b], 1u);
                 store_rec<T, kWords>(recs + (size_t)pos * kWords, rec);
@@ -435,12 +460,14 @@ __global__ __launch_bounds__(NT) void k_bucket_fill(EsParams<T> p,
 
 // Zero the grid cells of tiles that several work items share.
 template<typename T>
-__global__ __launch_bounds__(kThreads) void k_zero_shared_tiles(int G,
-        int ntiles, const uint32_t* __restrict__ item_start, T* grid)
+__global__ __launch_bounds__(kThreads) void k_zero_shared_tiles(
+        EsParams<T> p, const uint32_t* __restrict__ item_start, T* grid)
 {
     const int b = blockIdx.x;
     if (item_start[b + 1] - item_start[b] <= 1) return;
-    const int r0 = (b / ntiles) * kTile, c0 = (b % ntiles) * kTile;
+    int r0, c0;
+    tile_origin(p, b, r0, c0);
+    const int G = p.G;
     const int nr = min(kTile, G - r0), nc = min(kTile, G - c0);
     for (int k = threadIdx.x; k < nr * nc * 2; k += kThreads)
     {
@@ -561,7 +588,9 @@ __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
     const uint32_t e0 = bin_start[b] + piece * kPiece;
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
     const int half = p.G / 2;
-    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    int r0, c0;
+    tile_origin(p, b, r0, c0);
+    if (r0 >= p.G || c0 >= p.G) return;    // phantom tile
     const int tu0 = r0 - half, tv0 = c0 - half;   // signed coords of tile
     __syncthreads();
 
@@ -764,7 +793,9 @@ __global__ __launch_bounds__(256) void k_scatter_mfma(EsParams<float> p,
     const uint32_t e0 = bin_start[b] + piece * kPiece;
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
     const int half = p.G / 2;
-    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    int r0, c0;
+    tile_origin(p, b, r0, c0);
+    if (r0 >= p.G || c0 >= p.G) return;    // phantom tile
     const int tu0 = r0 - half, tv0 = c0 - half;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i = lane & 15, kq = lane >> 4;
@@ -988,7 +1019,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     const uint32_t e0 = bin_start[b] + piece * kPiece;
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
     const int half = p.G / 2;
-    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    int r0, c0;
+    tile_origin(p, b, r0, c0);
+    if (r0 >= p.G || c0 >= p.G) return;    // phantom tile
     const int tu0 = r0 - half, tv0 = c0 - half;
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
@@ -1218,7 +1251,9 @@ __global__ __launch_bounds__(256) void k_gather_mfma(EsParams<float> p,
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
     if (e0 >= e1) return;   // empty tile
     const int half = p.G / 2;
-    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    int r0, c0;
+    tile_origin(p, b, r0, c0);
+    if (r0 >= p.G || c0 >= p.G) return;    // phantom tile
     const int tu0 = r0 - half, tv0 = c0 - half;
     const float2* g2 = (const float2*)grid;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1370,7 +1405,9 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
     if (e0 >= e1) return;   // empty tile
     const int half = p.G / 2;
-    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    int r0, c0;
+    tile_origin(p, b, r0, c0);
+    if (r0 >= p.G || c0 >= p.G) return;    // phantom tile
     const int tu0 = r0 - half, tv0 = c0 - half;
     const float2* g2 = (const float2*)grid;
     const int t = threadIdx.x;
@@ -1539,7 +1576,9 @@ __global__ __launch_bounds__(kThreads) void k_gather(EsParams<T> p,
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
     if (e0 >= e1) return;   // empty tile: nothing to gather
     const int half = p.G / 2;
-    const int r0 = (b / p.ntiles) * kTile, c0 = (b % p.ntiles) * kTile;
+    int r0, c0;
+    tile_origin(p, b, r0, c0);
+    if (r0 >= p.G || c0 >= p.G) return;    // phantom tile
     const int tu0 = r0 - half, tv0 = c0 - half;
     using T2 = typename Vec2<T>::type;
     const T2* g2 = (const T2*)grid;
@@ -1824,8 +1863,9 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
     k_scan_columns<<<(p.nbins + 63) / 64, 1024, 0, stream>>>(
             s->table, nc, p.nbins, s->bin_count);
     SDP_HIP_CHECK_LAUNCH(status);
-    k_scan_bins<<<1, 1024, 0, stream>>>(s->bin_count, p.nbins, s->bin_start,
-            s->item_start, s->totals, s->item_bin, s->item_capacity);
+    k_scan_bins<<<1, 1024, 0, stream>>>(s->bin_count, p.nbins,
+            s->bin_start, s->item_start, s->totals, s->item_bin,
+            s->item_capacity);
     SDP_HIP_CHECK_LAUNCH(status);
     // No host round trip: records and work items are sized for the worst
     // case by the caller (BucketScratch::recs_bytes / item_capacity).
@@ -1880,7 +1920,7 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     sdp_Error st = SDP_SUCCESS;
     sdp_Error* status = &st;
     k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
-            p.G, p.ntiles, s.item_start, grid);
+            p, s.item_start, grid);
     SDP_HIP_CHECK_LAUNCH(status);
     if constexpr (sizeof(T) == 4)
     {

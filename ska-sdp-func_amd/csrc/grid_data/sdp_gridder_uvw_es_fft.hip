@@ -49,6 +49,8 @@ struct sdp_GridderUvwEsFft
     void* grid;                 // G x G complex plane
     void* tables;               // conv_corr | quad kernel | nodes | weights
     int ntiles;
+    int ncoarse;
+    int ncbins;
     int nbins;
     sdp_es::BucketScratch scratch;
     sdp_fft::Plan2D* fft;       // rocFFT (f64, or grids es_fft does not take)
@@ -257,6 +259,8 @@ sdp_es::EsParams<T> es_params(const sdp_GridderUvwEsFft* plan, int plane)
     p.do_w = plan->do_wstacking;
     p.plane = plane;
     p.ntiles = plan->ntiles;
+    p.ncoarse = plan->ncoarse;
+    p.ncbins = plan->ncbins;
     p.nbins = plan->nbins;
     p.beta = (T)plan->beta;
     p.uv_scale = (T)plan->uv_scale;
@@ -526,7 +530,10 @@ sdp_GridderUvwEsFft* sdp_gridder_uvw_es_fft_create_plan(
             plan->image_size, plan->grid_size, plan->support, plan->beta,
             host + nc, host + nc + q, host + nc + 2 * q, host);
     plan->ntiles = (plan->grid_size + sdp_es::kTile - 1) / sdp_es::kTile;
-    plan->nbins = plan->ntiles * plan->ntiles;
+    plan->ncoarse = (plan->grid_size + sdp_es::kCoarseTile - 1) /
+            sdp_es::kCoarseTile;
+    plan->ncbins = plan->ncoarse * plan->ncoarse;
+    plan->nbins = plan->ncbins * sdp_es::kCoarse * sdp_es::kCoarse;
     plan->stream = 0;
 
     if (!sdp_hip::device_available())

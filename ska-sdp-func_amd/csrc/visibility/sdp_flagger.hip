@@ -177,11 +177,6 @@ __device__ __forceinline__ void set_flag(int32_t* row, int j, int P, int lane)
     *(int32_t*)(base + (uint32_t)(lane * P) * 4u) = 1;
 }
 
-__device__ __forceinline__ int lane_prefix(uint64_t mask)
-{
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
 
 template<typename K, int N>
 __device__ __forceinline__ int count_lt(const K (&key)[N], K c)
