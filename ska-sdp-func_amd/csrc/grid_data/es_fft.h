@@ -48,8 +48,12 @@ int fft_twiddles_create(int grid_size, FftTwiddles* tw);
 void fft_twiddles_destroy(FftTwiddles* tw);
 
 // Gridding, part 1: row pass + first column pass (in place on grid).
+// tiles: nullptr (every cell of the grid is valid), or the bucketing's
+// per-tile entry counts (BucketScratch::bin_count, block-major bins of
+// 64 x 64 cells, ncoarse blocks per axis) when the scatter skipped the
+// empty tiles: the row pass then reads nothing of those (they are zero).
 int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
-        float* grid, hipStream_t stream);
+        float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream);
 // Gridding, part 2: last column pass + screen/correction into dirty.
 int fft_grid_to_image(const ImageParams<float>& ip, int plane,
         const FftTwiddles& tw, float* grid, float* dirty, hipStream_t stream);

@@ -512,21 +512,50 @@ constexpr uint32_t grid_bytes(int G, int k0)
 template<int G>
 __global__ void __launch_bounds__(RowPlan<G>::P)
 k_rows_grid(float2* __restrict__ grid, int k0, int M,
-        const float2* __restrict__ W)
+        const float2* __restrict__ W, const uint32_t* __restrict__ tiles,
+        int ncoarse)
 {
     using F = RowFft<G, 1>;
+    static_assert(F::EPT <= 32, "one mask bit per element");
     extern __shared__ float2 lds[];
     const int p = threadIdx.x;
     const Buf gb(grid - k0, grid_bytes(G, k0));
     F f;
     f.init(p, W, G);
-    for (int row = blockIdx.x; row < G; row += gridDim.x)
+    // Contiguous blocks of rows per workgroup (whole 64-row tile rows for
+    // the usual G / gridDim): the thread's element mask of occupied tiles
+    // is rebuilt only when the tile row changes. Element c of a thread
+    // (column p + c, c a multiple of P) is bit c / P.
+    const int per = (G + gridDim.x - 1) / gridDim.x;
+    const int r_begin = blockIdx.x * per, r_end = min(G, r_begin + per);
+    uint32_t occ = ~0u;
+    int occ_row = -1;
+    for (int row = r_begin; row < r_end; ++row)
     {
         const int pq = opaque(p);
+        if (tiles && (row >> 6) != occ_row)
+        {
+            // Tiles with no bucketed visibility were not written by the
+            // scatter (their cells are zero): read nothing for them.
+            occ_row = row >> 6;
+            occ = 0u;
+#pragma unroll
+            for (int b = 0; b < F::EPT; ++b)
+            {
+                const unsigned tu = (unsigned)occ_row;
+                const unsigned tv = (unsigned)(pq + b * RowPlan<G>::P) >> 6;
+                const unsigned bin = (((tu >> 2) * (unsigned)ncoarse +
+                        (tv >> 2)) << 4) | ((tu & 3u) << 2) | (tv & 3u);
+                if (tiles[bin] != 0u) occ |= 1u << b;
+            }
+        }
         const uint32_t vo = (uint32_t)pq * 8u;
         const uint32_t ro = ((uint32_t)row * G + k0) * 8u;
         float2 v[F::EPT];
-        F::load_input(v, [&](int c) { return gb.load(vo, ro + c * 8u); });
+        F::load_input(v, [&](int c) {
+            return gb.load_if((occ >> (c / RowPlan<G>::P)) & 1u,
+                    vo + ro + c * 8u);
+        });
         f.transform(v, pq, lds, RowIdx{});
         const uint32_t vr = (uint32_t)row * G * 8u + vo;
         F::store_output(v, [&](int c, int, float2 x) {
@@ -834,7 +863,7 @@ Geometry geometry(const ImageParams<float>& ip)
 
 template<int N1, int N2>
 int grid_rows_cols(const Geometry& g, const float2* W, float2* grid,
-        hipStream_t stream)
+        const uint32_t* tiles, int ncoarse, hipStream_t stream)
 {
     constexpr int G = N1 * N2;
     sdp_Error st = SDP_SUCCESS;
@@ -842,7 +871,7 @@ int grid_rows_cols(const Geometry& g, const float2* W, float2* grid,
     SDP_HIP_CHECK((allow_lds<k_rows_grid<G>>(lds)), &st);
     if (st) return st;
     k_rows_grid<G><<<row_blocks(G), RowPlan<G>::P, lds, stream>>>(
-            grid, g.k0, g.M, W);
+            grid, g.k0, g.M, W, tiles, ncoarse);
     SDP_HIP_CHECK_LAUNCH(&st);
     if (st) return st;
     k_cols_a_grid<N1, N2><<<col_grid(N1, g.M, ColPlan<N2>::B), 256,
@@ -953,12 +982,12 @@ void fft_twiddles_destroy(FftTwiddles* tw)
 }
 
 int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
-        float* grid, hipStream_t stream)
+        float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream)
 {
     const Geometry g = geometry(ip);
     const float2* W = (const float2*)tw.table;
     SDP_ES_FFT_DISPATCH(g.G, (grid_rows_cols<N1, N2>(g, W, (float2*)grid,
-            stream)))
+            tiles, ncoarse, stream)))
 }
 
 int fft_grid_to_image(const ImageParams<float>& ip, int plane,

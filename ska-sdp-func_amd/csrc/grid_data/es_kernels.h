@@ -81,10 +81,12 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
         BucketScratch* s, hipStream_t stream, uint32_t* n_entries,
         uint32_t* n_items);
 
-// Grid-mode tile accumulation: writes every cell of the G x G grid.
+// Grid-mode tile accumulation: writes every cell of the G x G grid, or
+// (skip_empty, f32 tap-table path) every cell of the tiles holding entries
+// -- for a consumer that reads the bin counts (fft_grid_rows_cols).
 template<typename T>
 int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
-        T* grid, hipStream_t stream);
+        T* grid, hipStream_t stream, bool skip_empty = false);
 
 // Degrid-mode tile gather: vis[idx] += sum_taps grid * kernel.
 template<typename T>

@@ -994,7 +994,8 @@ template<bool DO_W, int NTAP>
 __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
-        const uint32_t* __restrict__ item_bin, float* __restrict__ grid)
+        const uint32_t* __restrict__ item_bin, float* __restrict__ grid,
+        int skip_empty)
 {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     constexpr int kChunk = 256;           // one entry per thread
@@ -1018,6 +1019,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     const uint32_t npieces = item_start[b + 1] - item_start[b];
     const uint32_t e0 = bin_start[b] + piece * kPiece;
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
+    // An empty tile is left unwritten when its only reader, the fused FFT
+    // row pass, is told (from the bin counts) to take it as zeros.
+    if (skip_empty && e0 == e1 && npieces == 1) return;
     const int half = p.G / 2;
     int r0, c0;
     tile_origin(p, b, r0, c0);
@@ -1915,7 +1919,7 @@ bool use_tap_tables()
 
 template<typename T>
 int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
-        T* grid, hipStream_t stream)
+        T* grid, hipStream_t stream, bool skip_empty)
 {
     sdp_Error st = SDP_SUCCESS;
     sdp_Error* status = &st;
@@ -1929,16 +1933,20 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
             ;
         else if (p.support <= 8 && p.do_w)
             k_scatter_tab<true, 9><<<n_items, 256, 0, stream>>>(
-                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
+                    p, recs, s.bin_start, s.item_start, s.item_bin, grid,
+                    skip_empty ? 1 : 0);
         else if (p.support <= 8)
             k_scatter_tab<false, 9><<<n_items, 256, 0, stream>>>(
-                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
+                    p, recs, s.bin_start, s.item_start, s.item_bin, grid,
+                    skip_empty ? 1 : 0);
         else if (p.support <= 16 && p.do_w)
             k_scatter_tab<true, 17><<<n_items, 256, 0, stream>>>(
-                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
+                    p, recs, s.bin_start, s.item_start, s.item_bin, grid,
+                    skip_empty ? 1 : 0);
         else if (p.support <= 16)
             k_scatter_tab<false, 17><<<n_items, 256, 0, stream>>>(
-                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
+                    p, recs, s.bin_start, s.item_start, s.item_bin, grid,
+                    skip_empty ? 1 : 0);
         if (use_tap_tables() && p.support <= 16)
             ;
         else if (p.do_w)
@@ -2084,7 +2092,7 @@ int reverse_screen(const ImageParams<T>& ip, int plane, T* dirty,
             const T*, const T*, const T*, BucketScratch*, hipStream_t, \
             uint32_t*, uint32_t*); \
     template int scatter<T>(const EsParams<T>&, const BucketScratch&, \
-            uint32_t, T*, hipStream_t); \
+            uint32_t, T*, hipStream_t, bool); \
     template int gather<T>(const EsParams<T>&, const BucketScratch&, \
             uint32_t, const T*, T*, hipStream_t); \
     template int screen_corr_2d<T>(const ImageParams<T>&, const T*, T*, \

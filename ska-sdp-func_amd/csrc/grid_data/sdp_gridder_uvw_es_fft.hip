@@ -293,7 +293,7 @@ sdp_es::ImageParams<T> image_params(const sdp_GridderUvwEsFft* plan)
 template<typename T>
 void scatter_plane(sdp_GridderUvwEsFft* plan, int plane, int64_t rows,
         int chan, const T* uvw, const T* freq, const T* vis, const T* weight,
-        T* grid, sdp_Error* status)
+        T* grid, bool skip_empty, sdp_Error* status)
 {
     if (*status) return;
     const sdp_es::EsParams<T> p = es_params<T>(plan, plane);
@@ -303,17 +303,20 @@ void scatter_plane(sdp_GridderUvwEsFft* plan, int plane, int64_t rows,
             vis, weight, &plan->scratch, plan->stream, &n_entries, &n_items);
     if (e) { *status = (sdp_Error)e; return; }
     timing_mark(plan, 1);
-    e = sdp_es::scatter<T>(p, plan->scratch, n_items, grid, plan->stream);
+    e = sdp_es::scatter<T>(p, plan->scratch, n_items, grid, plan->stream,
+            skip_empty);
     if (e) { *status = (sdp_Error)e; return; }
     timing_mark(plan, 2);
 }
 
 // FFT of the gridded plane + image-plane step into dirty (per plane): the
 // fused pruned passes (f32, es_fft.h) or rocFFT + screen kernels.
+// sparse: the grid holds only the tiles of this plane's bucketing (the
+// scatter ran with skip_empty), the rest is implied zero.
 template<typename T>
 void grid_to_image(sdp_GridderUvwEsFft* plan,
         const sdp_es::ImageParams<T>& ip, int plane, T* grid, T* dirty,
-        sdp_Error* status)
+        bool sparse, sdp_Error* status)
 {
     if (*status) return;
     int e = 0;
@@ -322,7 +325,8 @@ void grid_to_image(sdp_GridderUvwEsFft* plan,
         if (plan->fused_fft)
         {
             e = sdp_es::fft_grid_rows_cols(ip, plan->fft_tw, grid,
-                    plan->stream);
+                    sparse ? plan->scratch.bin_count : nullptr,
+                    plan->ncoarse, plan->stream);
             if (e) { *status = (sdp_Error)e; return; }
             timing_mark(plan, 3);
             e = sdp_es::fft_grid_to_image(ip, plane, plan->fft_tw, grid,
@@ -380,9 +384,12 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
     T* grid = (T*)plan->grid;
     for (int plane = 0; plane < plan->num_total_w_grids && !*status; ++plane)
     {
+        // With the fused f32 FFT the empty tiles are neither written nor
+        // read (the row pass takes them from the bin counts as zeros).
+        const bool sparse = std::is_same<T, float>::value && plan->fused_fft;
         scatter_plane<T>(plan, plane, rows, chan, uvw, freq, vis, weight,
-                grid, status);
-        grid_to_image<T>(plan, ip, plane, grid, dirty, status);
+                grid, sparse, status);
+        grid_to_image<T>(plan, ip, plane, grid, dirty, sparse, status);
         if (*status) return;
         if (plan->do_wstacking && plane == plan->num_total_w_grids - 1)
         {
@@ -785,12 +792,12 @@ void sdp_grid_uvw_es_fft_scatter(sdp_GridderUvwEsFft* plan,
         scatter_plane<double>(plan, 0, rows, chan,
                 *(const double* const*)p_uvw, *(const double* const*)p_freq,
                 *(const double* const*)p_vis, *(const double* const*)p_wt,
-                *(double**)p_grid, status);
+                *(double**)p_grid, false, status);
     else
         scatter_plane<float>(plan, 0, rows, chan,
                 *(const float* const*)p_uvw, *(const float* const*)p_freq,
                 *(const float* const*)p_vis, *(const float* const*)p_wt,
-                *(float**)p_grid, status);
+                *(float**)p_grid, false, status);
 }
 
 void sdp_grid_uvw_es_fft_finish(sdp_GridderUvwEsFft* plan, sdp_Mem* grid,
@@ -823,10 +830,10 @@ void sdp_grid_uvw_es_fft_finish(sdp_GridderUvwEsFft* plan, sdp_Mem* grid,
     if (*status) return;
     if (plan->is_double)
         grid_to_image<double>(plan, image_params<double>(plan), 0,
-                *(double**)p_grid, *(double**)p_dirty, status);
+                *(double**)p_grid, *(double**)p_dirty, false, status);
     else
         grid_to_image<float>(plan, image_params<float>(plan), 0,
-                *(float**)p_grid, *(float**)p_dirty, status);
+                *(float**)p_grid, *(float**)p_dirty, false, status);
 }
 
 } // extern "C"
