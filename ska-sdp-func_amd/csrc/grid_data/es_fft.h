@@ -63,9 +63,11 @@ int fft_grid_to_image(const ImageParams<float>& ip, int plane,
 int fft_image_cols(const ImageParams<float>& ip, int plane,
         const FftTwiddles& tw, float* dirty, bool correct_in_place,
         float* grid, hipStream_t stream);
-// Degridding, part 2: second column pass + row pass writing every grid cell.
+// Degridding, part 2: second column pass + row pass writing the grid:
+// every cell (tiles == nullptr), or only the tiles the gather of this
+// bucketing reads (tiles = BucketScratch::bin_count of the degrid bins).
 int fft_image_to_grid(const ImageParams<float>& ip, const FftTwiddles& tw,
-        float* grid, hipStream_t stream);
+        float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream);
 
 } // namespace sdp_es
 

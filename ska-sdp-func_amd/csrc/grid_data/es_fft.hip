@@ -779,17 +779,48 @@ k_cols_b_image(float2* __restrict__ grid, int M, const float2* __restrict__ W)
 template<int G>
 __global__ void __launch_bounds__(RowPlan<G>::P)
 k_rows_image(float2* __restrict__ grid, int k0, int M,
-        const float2* __restrict__ W)
+        const float2* __restrict__ W, const uint32_t* __restrict__ tiles,
+        int ncoarse)
 {
     using F = RowFft<G, -1>;
+    constexpr int P = RowPlan<G>::P;
+    static_assert(F::EPT <= 32, "one mask bit per element");
     extern __shared__ float2 lds[];
     const int p = threadIdx.x;
     const Buf gb(grid - k0, grid_bytes(G, k0));
     F f;
     f.init(p, W, G);
-    for (int row = blockIdx.x; row < G; row += gridDim.x)
+    // As k_rows_grid: contiguous row blocks and a per-thread element mask,
+    // here of the tiles the gather will read -- tile (tu, tv) is read by
+    // the visibilities bucketed in it and (halo, taps reach <= 16 cells
+    // past a tile) in the tiles above and to the left of it.
+    const int per = (G + gridDim.x - 1) / gridDim.x;
+    const int r_begin = blockIdx.x * per, r_end = min(G, r_begin + per);
+    const int nt = G / kTile;
+    auto count = [&](int tu, int tv) -> uint32_t {
+        if (tu < 0 || tv < 0) return 0u;
+        const unsigned u = (unsigned)tu, v = (unsigned)tv;
+        return tiles[(((u >> 2) * (unsigned)ncoarse + (v >> 2)) << 4) |
+                ((u & 3u) << 2) | (v & 3u)];
+    };
+    uint32_t need = ~0u;
+    int need_row = -1;
+    for (int row = r_begin; row < r_end; ++row)
     {
         const int pq = opaque(p);
+        if (tiles && (row >> 6) != need_row)
+        {
+            need_row = row >> 6;
+            need = 0u;
+#pragma unroll
+            for (int b = 0; b < F::EPT; ++b)
+            {
+                const int tu = need_row, tv = (pq + b * P) >> 6;
+                if (tv < nt && (count(tu, tv) | count(tu - 1, tv) |
+                        count(tu, tv - 1) | count(tu - 1, tv - 1)))
+                    need |= 1u << b;
+            }
+        }
         const uint32_t vo = (uint32_t)pq * 8u;
         const uint32_t rs = (uint32_t)row * G * 8u;
         float2 v[F::EPT];
@@ -801,7 +832,9 @@ k_rows_image(float2* __restrict__ grid, int k0, int M,
         f.transform(v, pq, lds, RowIdx{});
         const uint32_t ro = ((uint32_t)row * G + k0) * 8u;
         F::store_output(v, [&](int c, int, float2 x) {
-            gb.store(x, vo, ro + c * 8u);
+            // Output element c of the thread is column p + c (c / P its
+            // mask bit); tiles nobody reads are not written.
+            gb.store_if((need >> (c / P)) & 1u, x, vo + ro + c * 8u);
         });
     }
 }
@@ -915,7 +948,7 @@ int image_cols(const Geometry& g, const ImageParams<float>& ip, int plane,
 
 template<int N1, int N2>
 int image_to_grid(const Geometry& g, const float2* W, float2* grid,
-        hipStream_t stream)
+        const uint32_t* tiles, int ncoarse, hipStream_t stream)
 {
     constexpr int G = N1 * N2;
     sdp_Error st = SDP_SUCCESS;
@@ -927,7 +960,7 @@ int image_to_grid(const Geometry& g, const float2* W, float2* grid,
     SDP_HIP_CHECK((allow_lds<k_rows_image<G>>(lds)), &st);
     if (st) return st;
     k_rows_image<G><<<row_blocks(G), RowPlan<G>::P, lds, stream>>>(
-            grid, g.k0, g.M, W);
+            grid, g.k0, g.M, W, tiles, ncoarse);
     SDP_HIP_CHECK_LAUNCH(&st);
     return st;
 }
@@ -1010,12 +1043,12 @@ int fft_image_cols(const ImageParams<float>& ip, int plane,
 }
 
 int fft_image_to_grid(const ImageParams<float>& ip, const FftTwiddles& tw,
-        float* grid, hipStream_t stream)
+        float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream)
 {
     const Geometry g = geometry(ip);
     const float2* W = (const float2*)tw.table;
     SDP_ES_FFT_DISPATCH(g.G, (image_to_grid<N1, N2>(g, W, (float2*)grid,
-            stream)))
+            tiles, ncoarse, stream)))
 }
 
 } // namespace sdp_es

@@ -361,8 +361,9 @@ void image_to_grid(sdp_GridderUvwEsFft* plan,
                     !plan->do_wstacking, grid, plan->stream);
             if (e) { *status = (sdp_Error)e; return; }
             timing_mark(plan, 2);
+            // Only the tiles this plane's gather reads are written.
             e = sdp_es::fft_image_to_grid(ip, plan->fft_tw, grid,
-                    plan->stream);
+                    plan->scratch.bin_count, plan->ncoarse, plan->stream);
             if (e) *status = (sdp_Error)e;
             return;
         }
