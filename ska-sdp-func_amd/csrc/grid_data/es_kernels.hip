@@ -1125,12 +1125,12 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 lcnt[cblk] += (int)__popcll(m);
             }
         }
-        // Pad every list to a multiple of 16 visits with the padding visit,
-        // so the matrix loop needs no bounds checks.
+        // Pad every list to a multiple of 4 visits (one matrix op) with the
+        // padding visit, so the matrix loop needs no bounds checks.
 #pragma unroll
         for (int cblk = 0; cblk < 4; ++cblk)
         {
-            const int pad = ((lcnt[cblk] + 15) & ~15) - lcnt[cblk];
+            const int pad = ((lcnt[cblk] + 3) & ~3) - lcnt[cblk];
             if (lane < pad) s_list[wave][cblk][lcnt[cblk] + lane] = kChunk;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1138,13 +1138,31 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
 #pragma unroll
         for (int cblk = 0; cblk < 4; ++cblk)
         {
-            const int cnt = __builtin_amdgcn_readfirstlane(
-                    (lcnt[cblk] + 15) & ~15);
+            const int cnt4 = __builtin_amdgcn_readfirstlane(
+                    (lcnt[cblk] + 3) & ~3);
+            const int cnt = cnt4 & ~15;
             const uint16_t* list = s_list[wave][cblk];
             const int base_v = cblk * 16 + i + 32;
             // The loop carries only this block's two accumulators (keeps
             // the register allocator from rotating the AGPRs of all four).
             f32x4 re = acc_re[cblk], im = acc_im[cblk];
+            // Tail first: the last (cnt4 - cnt) / 4 groups of four visits,
+            // one matrix op each.
+            for (int g = cnt; g < cnt4; g += 4)
+            {
+                const uint32_t q = s_info[list[g + kq]];
+                const int e = (int)(q & 0xffu);
+                const int du = base_u - (int)((q >> 8) & 0xffu);
+                const int dv = base_v - (int)((q >> 16) & 0xffu);
+                const int ia = ((unsigned)du < (unsigned)NTAP) ?
+                        e * NTAP + du : kZero;
+                const int ib = ((unsigned)dv < (unsigned)NTAP) ?
+                        e * NTAP + dv : kZero;
+                const float a = s_ku[ia];
+                const float2 bb = s_kv[ib];
+                re = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.x, re, 0, 0, 0);
+                im = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.y, im, 0, 0, 0);
+            }
             // Four groups of four visits per step: all LDS reads of a step
             // are issued before the first matrix op waits on them.
             for (int g = 0; g < cnt; g += 16)
