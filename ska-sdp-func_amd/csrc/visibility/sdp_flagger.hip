@@ -178,12 +178,22 @@ __device__ __forceinline__ void set_flag(int32_t* row, int j, int P, int lane)
 }
 
 
+// Key sets: key(j), j < N, from a register array or computed on the fly
+// (a statistic's keys are then never held as an array: they are rebuilt in
+// the bracket pass and, rarely, in the full search).
 template<typename K, int N>
-__device__ __forceinline__ int count_lt(const K (&key)[N], K c)
+struct ArrayKeys
+{
+    const K (&a)[N];
+    __device__ __forceinline__ K operator()(int j) const { return a[j]; }
+};
+
+template<typename K, int N, class Keys>
+__device__ __forceinline__ int count_lt(const Keys& key, K c)
 {
     int s = 0;
 #pragma unroll
-    for (int j = 0; j < N; ++j) s += __popcll(ballot(key[j] < c));
+    for (int j = 0; j < N; ++j) s += __popcll(ballot(key(j) < c));
     return s;
 }
 
@@ -191,8 +201,8 @@ __device__ __forceinline__ int count_lt(const K (&key)[N], K c)
 // keys). Without it L and U are implied by prefix and bit, which holds
 // when the set lies inside [prefix, prefix + 2^(bit+1)) -- true of the
 // compacted bracket candidates -- and a probe is one counting pass.
-template<typename K, int N, bool CHECKS>
-__device__ __forceinline__ K search(const K (&key)[N], int k, K prefix,
+template<typename K, int N, bool CHECKS, class Keys>
+__device__ __forceinline__ K search(const Keys& key, int k, K prefix,
         int bit, K L, K U, int c0, int c1, int& nprobe)
 {
     while (c1 - c0 > 1 && bit >= 0)
@@ -230,10 +240,21 @@ __device__ __forceinline__ K search(const K (&key)[N], int k, K prefix,
 #pragma unroll
     for (int j = 0; j < N; ++j)
     {
-        const uint64_t m = ballot(key[j] >= L) & ballot(key[j] < U);
-        if (m) ans = readlane(key[j], (int)__builtin_ctzll(m));
+        const K kj = key(j);
+        const uint64_t m = ballot(kj >= L) & ballot(kj < U);
+        if (m) ans = readlane(kj, (int)__builtin_ctzll(m));
     }
     return ans;
+}
+
+// Wave-uniform double in scalar registers.
+__device__ __forceinline__ double uniform(double x)
+{
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)(uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
 #ifdef SDP_FLAGGER_STATS
@@ -248,10 +269,10 @@ struct Track
     bool valid;
 };
 
-template<typename V, int N, int R>
-__device__ __forceinline__ V select_tracked(
-        const typename KeyOf<V>::type (&key)[N], int k, int nvalid,
-        Track& tr, typename KeyOf<V>::type* cand_lds, int lane, int sid)
+template<typename V, int N, int R, class Keys>
+__device__ __forceinline__ V select_tracked(const Keys& key, int k,
+        int nvalid, Track& tr, typename KeyOf<V>::type* cand_lds, int lane,
+        int sid)
 {
     using K = typename KeyOf<V>::type;
     constexpr int kTop = KeyOf<V>::kTop;
@@ -286,16 +307,16 @@ __device__ __forceinline__ V select_tracked(
 #pragma unroll
             for (int j = 0; j < N; ++j)
             {
-                const uint64_t mb = ballot(key[j] < lo);
-                const uint64_t mi = ballot(key[j] <= hi) & ~mb;
+                const K kj = key(j);
+                const uint64_t mb = ballot(kj < lo);
+                const uint64_t mi = ballot(kj <= hi) & ~mb;
                 if (kCompact)
                 {
                     const uint32_t pos = __builtin_amdgcn_mbcnt_hi(
                             (uint32_t)(mi >> 32), __builtin_amdgcn_mbcnt_lo(
                             (uint32_t)mi, (uint32_t)n_in));
                     const bool inside = __builtin_amdgcn_inverse_ballot_w64(mi);
-                    cand_lds[inside && pos < (uint32_t)kCap ? pos : kCap] =
-                            key[j];
+                    cand_lds[inside && pos < (uint32_t)kCap ? pos : kCap] = kj;
                 }
                 c_lt += __popcll(mb);
                 n_in += __popcll(mi);
@@ -357,14 +378,16 @@ __device__ __forceinline__ V select_tracked(
             const int s = lane + 64 * r;
             c[r] = s < n_in ? cand_lds[s] : ~(K)0;
         }
-        ans = search<K, kCompact ? R : 1, false>(c, kk, prefix, bit, L, U,
-                c0, c1, nprobe);
+        ans = search<K, kCompact ? R : 1, false>(
+                ArrayKeys<K, kCompact ? R : 1>{c}, kk, prefix, bit, L, U, c0,
+                c1, nprobe);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
     else
     {
-        ans = search<K, N, true>(key, kk, prefix, bit, L, U, c0, c1, nprobe);
+        ans = search<K, N, true>(key, kk, prefix, bit, L, U, c0, c1,
+                nprobe);
     }
 
     // Bracket for the next time step: centred on this value, half-width
@@ -405,6 +428,7 @@ __device__ __forceinline__ V select_tracked(
     if (!(tr.w <= fabs(a) * 1024.0)) tr.w = fabs(a) * 1024.0;
     if (!(tr.w >= 0.0)) tr.w = 0.0;
     tr.x = a;
+    tr.w = uniform(tr.w);         // bracket state stays in scalar registers
     tr.valid = isfinite(a);
     return val_of(ans);
 }
@@ -582,23 +606,34 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
         for (int j = 0; j < EPL; ++j)
             m[j] = ch_ok[j] ? (FP)mag_of(raw[j].x, raw[j].y) : (FP)0;
         if (t + 1 < prm.T) load_step(t + 1, P, lane);
+        // Transit update first (:262-274), so the previous magnitudes are
+        // dead before the selections and share registers with m.
+        if (t > 0)
+        {
+#pragma unroll
+            for (int j = 0; j < EPL; ++j)
+            {
+                const double rate = fabs((double)prev[j] - (double)m[j]);
+                transit[j] = (t == 1) ? rate :
+                        prm.alpha * rate + (1 - prm.alpha) * transit[j];
+            }
+        }
 
         // Magnitude median and MAD over the sampled channels (:170-178).
         double median, mediandev;
         {
-            KM km[EPL];
-#pragma unroll
-            for (int j = 0; j < EPL; ++j)
-                km[j] = smp_ok[j] ? key_of(m[j]) : ~(KM)0;
+            auto km = [&](int j) -> KM {
+                return smp_ok[j] ? key_of(m[j]) : ~(KM)0;
+            };
             median = (double)select_tracked<FP, EPL, kCandRegs>(km, k_s,
                     prm.ns, tk_mag, (KM*)cand, lane, 0);
         }
         {
-            uint64_t kd[EPL];
-#pragma unroll
-            for (int j = 0; j < EPL; ++j)
-                kd[j] = smp_ok[j] ? key_of(fabs((double)m[j] - median)) :
-                                    ~(uint64_t)0;
+            // |m - median| keys, rebuilt wherever they are read.
+            auto kd = [&](int j) -> uint64_t {
+                return smp_ok[j] ? key_of(fabs((double)m[j] - median)) :
+                                   ~(uint64_t)0;
+            };
             mediandev = select_tracked<double, EPL, kCandRegs>(kd, k_s,
                     prm.ns, tk_dev, (uint64_t*)cand, lane, 1);
         }
@@ -622,14 +657,16 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
             }
             const int k_h = mid_index(medwindow);
             const double medmed = select_tracked<double, HEPL, kCandRegs>(
-                    hk, k_h, medwindow, tk_h, (uint64_t*)cand, lane, 2);
+                    ArrayKeys<uint64_t, HEPL>{hk}, k_h, medwindow, tk_h,
+                    (uint64_t*)cand, lane, 2);
 #pragma unroll
             for (int j = 0; j < HEPL; ++j)
             {
                 if (hk[j] != ~(uint64_t)0) hk[j] = key_of(fabs(hv[j] - medmed));
             }
             const double medmeddev = select_tracked<double, HEPL, kCandRegs>(
-                    hk, k_h, medwindow, tk_hdev, (uint64_t*)cand, lane, 3);
+                    ArrayKeys<uint64_t, HEPL>{hk}, k_h, medwindow, tk_hdev,
+                    (uint64_t*)cand, lane, 3);
             const double zmed = modified_zscore(medmed, medmeddev, median);
             situation = zmed > prm.thr_bb || zmed < -prm.thr_bb;
         }
@@ -652,29 +689,20 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
         // Fluctuations (:245-339).
         if (t > 0)
         {
-#pragma unroll
-            for (int j = 0; j < EPL; ++j)
-            {
-                const double rate = fabs((double)prev[j] - (double)m[j]);
-                transit[j] = (t == 1) ? rate :
-                        prm.alpha * rate + (1 - prm.alpha) * transit[j];
-            }
             double medianvar, mediandevvar;
             {
-                uint64_t kt[EPL];
-#pragma unroll
-                for (int j = 0; j < EPL; ++j)
-                    kt[j] = smp_ok[j] ? key_of(transit[j]) : ~(uint64_t)0;
+                auto kt = [&](int j) -> uint64_t {
+                    return smp_ok[j] ? key_of(transit[j]) : ~(uint64_t)0;
+                };
                 medianvar = select_tracked<double, EPL, kCandRegs>(kt, k_s,
                         prm.ns, tk_var, (uint64_t*)cand, lane, 4);
             }
             {
                 // MAD around the MAGNITUDE median (:292-295).
-                uint64_t kv[EPL];
-#pragma unroll
-                for (int j = 0; j < EPL; ++j)
-                    kv[j] = smp_ok[j] ? key_of(fabs(transit[j] - median)) :
-                                        ~(uint64_t)0;
+                auto kv = [&](int j) -> uint64_t {
+                    return smp_ok[j] ? key_of(fabs(transit[j] - median)) :
+                                       ~(uint64_t)0;
+                };
                 // |transit - median| sits about `median` above zero: move
                 // its bracket with the magnitude median.
                 if (tk_vdev.valid) tk_vdev.x += median - prev_median;
