@@ -35,20 +35,24 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--window", type=int, default=0)
     ap.add_argument("--step", type=int, default=1)
+    ap.add_argument("--dtype", choices=("c64", "c128"), default="c64")
     ap.add_argument("--cpu-sample-baselines", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
 
-def make_vis(torch, dev, T, B, C, P, seed):
+def make_vis(torch, dev, T, B, C, P, seed, dtype):
     """1+1j + 0.05 complex noise, planted narrowband / broadband RFI,
     generated time step by time step in HBM."""
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
-    vis = torch.empty((T, B, C, P), dtype=torch.complex64, device=dev)
+    vis = torch.empty((T, B, C, P), dtype=dtype, device=dev)
+    real = torch.float32 if dtype == torch.complex64 else torch.float64
     for t in range(T):
-        re = torch.randn((B, C, P), generator=g, device=dev) * 0.05 + 1.0
-        im = torch.randn((B, C, P), generator=g, device=dev) * 0.05 + 1.0
+        re = torch.randn((B, C, P), generator=g, device=dev,
+                         dtype=real) * 0.05 + 1.0
+        im = torch.randn((B, C, P), generator=g, device=dev,
+                         dtype=real) * 0.05 + 1.0
         vis[t] = torch.complex(re, im)
     n_nb = max(1, T * B * P // 20)
     idx = [torch.randint(0, n, (n_nb,), generator=g, device=dev)
@@ -88,7 +92,9 @@ def main():
 
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    vis = make_vis(torch, dev, args.T, args.B, args.C, args.P, 20251015 + 5)
+    cdt = torch.complex64 if args.dtype == "c64" else torch.complex128
+    vis = make_vis(torch, dev, args.T, args.B, args.C, args.P, 20251015 + 5,
+                   cdt)
     flags = torch.zeros(vis.shape, dtype=torch.int32, device=dev)
     kw = dict(alpha=0.5, threshold_magnitudes=3.5, threshold_variations=3.5,
               threshold_broadband=3.5, sampling_step=args.step,
@@ -104,7 +110,7 @@ def main():
     n = vis.numel()
     value = n / dt / 1e6
     flagged = float(flags.sum(dtype=torch.int64).item()) / n
-    algo = 12 * n
+    algo = (vis.element_size() + 4) * n   # visibility read + int32 flag write
     achieved = algo / dt / 1e9
     cpu = None if args.no_cpu_baseline else cpu_baseline(vis, args, kw)
     line = {
@@ -118,11 +124,11 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "c64 in, f64 statistics, int32 flags",
+        "dtype": f"{args.dtype} in, f64 statistics, int32 flags",
         "data": "synthetic (config-5 shape, planted RFI, generated in HBM)",
         "config": {"workload": (f"sdp_flagger_dynamic_threshold vis "
                                 f"[{args.T}, {args.B}, {args.C}, {args.P}] "
-                                f"c64, step {args.step}, window "
+                                f"{args.dtype}, step {args.step}, window "
                                 f"{args.window}, history 20"),
                    "flagged_fraction": round(flagged, 5)},
         "roofline": {"kernel": "k_flagger (wave per baseline stream)",

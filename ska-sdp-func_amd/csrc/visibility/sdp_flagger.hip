@@ -512,8 +512,12 @@ __device__ __forceinline__ bool spread(const uint8_t* trig, int d, int C,
 // Tuning hook: e.g. -DFLAGGER_WAVES="__attribute__((amdgpu_waves_per_eu(3)))"
 // (measured: 3 or 4 waves per SIMD by spilling ran 2-6 % slower than the
 // compiler's own allocation at config 5).
+// Occupancy targets: the float kernels fit 128 VGPRs (4 waves per SIMD) with
+// a few dwords of spill, which measures faster than 3 waves without; the
+// double kernels (two registers per statistic key) stay at 3.
 #ifndef FLAGGER_WAVES
-#define FLAGGER_WAVES
+#define FLAGGER_WAVES \
+    __attribute__((amdgpu_waves_per_eu(sizeof(FP) == 4 ? 4 : 3)))
 #endif
 constexpr int kCandRegs = 3;      // compacted candidates: 192 per statistic
 
@@ -572,8 +576,9 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
 
     const int64_t time_block = prm.B * (int64_t)C * prm.P;
     const int64_t stream_off = b * (int64_t)C * prm.P + p;
-    // Visibilities of the next time step are loaded while the current one
-    // is processed (one complex value per register slot).
+    // One complex value per register slot. Latency is hidden by occupancy
+    // (4 streams per SIMD) rather than by a register prefetch of the next
+    // step, which would cost 32 registers and a wave per SIMD.
     typedef FP FP2 __attribute__((ext_vector_type(2)));
     FP2 raw[EPL];
     auto load_step = [&](int64_t tt, int P, int lane) {
@@ -589,7 +594,6 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
             }
         }
     };
-    load_step(0, prm.P, lane0);
     double prev_median = 0.0;
     for (int64_t t = 0; t < prm.T; ++t)
     {
@@ -602,10 +606,10 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
         const int64_t row = t * time_block + stream_off;
         int32_t* frow = flags + row;
         int32_t* fprev = frow - time_block;
+        load_step(t, P, lane);
 #pragma unroll
         for (int j = 0; j < EPL; ++j)
             m[j] = ch_ok[j] ? (FP)mag_of(raw[j].x, raw[j].y) : (FP)0;
-        if (t + 1 < prm.T) load_step(t + 1, P, lane);
         // Transit update first (:262-274), so the previous magnitudes are
         // dead before the selections and share registers with m.
         if (t > 0)
