@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "ska-sdp-func_amd"))
 sys.path.insert(0, ROOT)
 
 C_0 = 299792458.0
-HBM_PEAK_GBS = 8000.0
+F32_PEAK_TFLOPS = 157.3
 KW = dict(support=8, oversampling=16384, w_support=8, w_oversampling=16384)
 
 
@@ -130,6 +130,27 @@ def cpu_baseline(uvw_dev, vis_dev, args, theta, w_step, H):
                        f"{args.image}^2 FFT and correction are excluded")}
 
 
+def roofline(tm, kernel):
+    """Roofline object of a fused tower kernel from the library's event
+    timing. Algorithmic flops (w-towers): every
+    visibility updates all S^2 pixels of its sub-grid image by a complex
+    rank-1 term (8 flops per pixel) and every sub-grid w-layer steps the
+    S^2-pixel Horner recurrence (one complex multiply-add, 8 flops per
+    pixel); bound: f32 matrix/vector peak (both 157.3 TFLOP/s on MI355X)."""
+    if not tm or not tm["launches"] or tm["kernel_ms"] <= 0:
+        return None
+    s2 = tm["subgrid_size"] ** 2
+    flops = 8.0 * s2 * (tm["vis"] + tm["layers"]) / tm["launches"]
+    avg_s = tm["kernel_ms"] * 1e-3 / tm["launches"]
+    achieved = flops / avg_s / 1e12
+    return {"kernel": kernel, "bound": "mfma",
+            "achieved": round(achieved, 2), "peak": F32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / F32_PEAK_TFLOPS, 4),
+            "traffic": None, "avg_launch_ms": round(1e3 * avg_s, 3),
+            "launches": tm["launches"],
+            "algorithmic_flops_per_launch": flops}
+
+
 def main():
     args = parse()
     import torch
@@ -178,6 +199,15 @@ def main():
         t_grid = float(t.item())
     total_vis = args.rows * args.chan
     value = total_vis * args.steps / t_grid / 1e6
+
+    # Roofline of the dominant kernel (k_tower_dft), timed by HIP events
+    # around each launch inside the library, in a separate step so that the
+    # event synchronisation stays out of the timed loop.
+    g.wstack_wtower_enable_timing(True)
+    grid_step()
+    barrier()
+    roof = roofline(g.wstack_wtower_get_timing(), "k_tower_dft")
+    g.wstack_wtower_enable_timing(False)
     if args.verbosity:
         grid_step(args.verbosity)
         barrier()
@@ -195,8 +225,14 @@ def main():
                                           world)
         barrier()
         t_deg = time.perf_counter() - t0
+        g.wstack_wtower_enable_timing(True)
+        g.wstack_wtower_degrid_planes(image, *common, 0, out, rank, world)
+        barrier()
+        droof = roofline(g.wstack_wtower_get_timing(), "k_tower_idft")
+        g.wstack_wtower_enable_timing(False)
         degrid = {"mvis_s": round(total_vis * args.steps / t_deg / 1e6, 3),
-                  "ms_per_step": round(1e3 * t_deg / args.steps, 2)}
+                  "ms_per_step": round(1e3 * t_deg / args.steps, 2),
+                  "roofline": droof}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -229,6 +265,7 @@ def main():
                 "w_tower_height": H,
                 "parallelism": f"w-stack planes / {world}",
             },
+            "roofline": roof,
             "degrid": degrid,
             "cpu_baseline": cpu,
         }

@@ -131,6 +131,18 @@ void sdp_grid_wstack_wtower_degrid_planes(
         sdp_Error* status
 );
 
+/* Device timing of the fused tower kernels (k_tower_dft when gridding,
+ * k_tower_idft when degridding) accumulated over the calls made while
+ * enabled: HIP events around every launch. enable_timing(1) switches it on
+ * and resets the totals; get_timing writes up to max_values of
+ * [0] total kernel time (ms), [1] launches, [2] visibilities gridded or
+ * degridded by the fused kernels, [3] sub-grid w-layers they stepped
+ * through, [4] sub-grid size, [5] 0 gridding / 1 degridding (last call)
+ * and returns the number written (0 if timing is off). Extension with no
+ * reference counterpart: the reference has no device path to time. */
+void sdp_grid_wstack_wtower_enable_timing(int enable);
+int sdp_grid_wstack_wtower_get_timing(double* out, int max_values);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1873,6 +1873,56 @@ struct Timing
     int64_t layers = 0;
 };
 
+// Device timing of the fused tower kernels (k_tower_dft / k_tower_idft),
+// switched on by sdp_grid_wstack_wtower_enable_timing: one HIP event pair
+// per launch on the launch stream, read back at the end of the call, plus
+// the work counts the roofline needs (visibilities, sub-grid w-layers).
+struct TowerTiming
+{
+    bool on = false;
+    std::vector<hipEvent_t> ev;     // start/stop pairs, reused across calls
+    size_t used = 0;
+    double ms = 0;
+    int64_t launches = 0, vis = 0, layers = 0;
+    int S = 0, kind = 0;            // kind: 0 gridding, 1 degridding
+
+    void start()
+    {
+        if (!on) return;
+        while (ev.size() < used + 2)
+        {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) { on = false; return; }
+            ev.push_back(e);
+        }
+        (void)hipEventRecord(ev[used], 0);
+    }
+    void stop()
+    {
+        if (!on || ev.size() < used + 2) return;
+        (void)hipEventRecord(ev[used + 1], 0);
+        used += 2;
+        ++launches;
+    }
+    void collect()
+    {
+        for (size_t i = 0; i + 1 < used; i += 2)
+        {
+            float t = 0.f;
+            if (hipEventSynchronize(ev[i + 1]) == hipSuccess &&
+                    hipEventElapsedTime(&t, ev[i], ev[i + 1]) == hipSuccess)
+                ms += t;
+        }
+        used = 0;
+    }
+};
+
+TowerTiming& tower_timing()
+{
+    static TowerTiming t;
+    return t;
+}
+
 
 // Grid all visibilities of the selected w-stack planes.
 template<typename T, typename U>
@@ -1975,9 +2025,11 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                 dp.w_kernel = k->d_w_kernel;
                 dp.tw = dd.tw;
                 const int tiles = (g.S / kDftTile) * (g.S / kDftTile);
+                tower_timing().start();
                 k_tower_dft<U><<<dim3(tiles, (unsigned)gr.slots), 256>>>(dp,
                         d_uvw, (const Cx<float>*)d_vis);
                 SDP_HIP_CHECK_LAUNCH(status);
+                tower_timing().stop();
                 sdp_fft::exec_2d(sp, d_stack, true, 0, status);
             }
             tm.layers += (gr.last_p - gr.first_p + ws_n) * gr.slots;
@@ -2058,6 +2110,15 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                 tm.image += now_s() - ti;
             }
         }
+    }
+    if (tower_timing().on && g.fused)
+    {
+        TowerTiming& tt = tower_timing();
+        tt.collect();
+        tt.vis += dd.n_vis;
+        tt.layers += tm.layers;
+        tt.S = g.S;
+        tt.kind = 0;
     }
     if (verbosity > 0 && !*status)
     {
@@ -2194,9 +2255,11 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
                 dp.tw = dd.tw;
                 dp.in = (const Cx<float>*)d_wimg;
                 dp.part = d_part;
+                tower_timing().start();
                 k_tower_idft<U><<<dim3(ntiles, (unsigned)gr.slots), 256>>>(
                         dp, d_uvw);
                 SDP_HIP_CHECK_LAUNCH(status);
+                tower_timing().stop();
             }
             tm.layers += (last - first + ws_n) * gr.slots;
             if (verbosity > 0)
@@ -2254,6 +2317,15 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
                     d_part, ntiles, g.num_chan, (Cx<float>*)d_vis);
             SDP_HIP_CHECK_LAUNCH(status);
         }
+    }
+    if (tower_timing().on && g.fused)
+    {
+        TowerTiming& tt = tower_timing();
+        tt.collect();
+        tt.vis += dd.n_vis;
+        tt.layers += tm.layers;
+        tt.S = g.S;
+        tt.kind = 1;
     }
     if (verbosity > 0 && !*status)
     {
@@ -2512,6 +2584,28 @@ void sdp_grid_wstack_wtower_degrid_planes(const sdp_Mem* image,
             shear_u, shear_v, support, oversampling, w_support,
             w_oversampling, subgrid_frac, w_tower_height, verbosity, vis,
             plane_offset, plane_stride, status);
+}
+
+void sdp_grid_wstack_wtower_enable_timing(int enable)
+{
+    TowerTiming& tt = tower_timing();
+    tt.collect();
+    tt.on = enable != 0;
+    tt.ms = 0;
+    tt.launches = tt.vis = tt.layers = 0;
+    tt.S = tt.kind = 0;
+}
+
+int sdp_grid_wstack_wtower_get_timing(double* out, int max_values)
+{
+    TowerTiming& tt = tower_timing();
+    if (!tt.on || !out) return 0;
+    tt.collect();
+    const double v[6] = {tt.ms, (double)tt.launches, (double)tt.vis,
+            (double)tt.layers, (double)tt.S, (double)tt.kind};
+    const int n = max_values < 6 ? max_values : 6;
+    for (int i = 0; i < n; ++i) out[i] = v[i];
+    return n;
 }
 
 } // extern "C"

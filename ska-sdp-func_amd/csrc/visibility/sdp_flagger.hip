@@ -509,17 +509,17 @@ __device__ __forceinline__ bool spread(const uint8_t* trig, int d, int C,
     return f;
 }
 
-// Tuning hook: e.g. -DFLAGGER_WAVES="__attribute__((amdgpu_waves_per_eu(3)))"
-// (measured: 3 or 4 waves per SIMD by spilling ran 2-6 % slower than the
-// compiler's own allocation at config 5).
-// Occupancy targets: the float kernels fit 128 VGPRs (4 waves per SIMD) with
+// Occupancy targets (tuning hook: -DFLAGGER_WAVES=...): the float kernels fit 128 VGPRs (4 waves per SIMD) with
 // a few dwords of spill, which measures faster than 3 waves without; the
 // double kernels (two registers per statistic key) stay at 3.
 #ifndef FLAGGER_WAVES
 #define FLAGGER_WAVES \
     __attribute__((amdgpu_waves_per_eu(sizeof(FP) == 4 ? 4 : 3)))
 #endif
-constexpr int kCandRegs = 3;      // compacted candidates: 192 per statistic
+#ifndef FLAGGER_CAND_REGS
+#define FLAGGER_CAND_REGS 2
+#endif
+constexpr int kCandRegs = FLAGGER_CAND_REGS;   // compacted candidates: 64 per register
 
 // Per-wave LDS layout: median history | trigger bytes (all, variation) |
 // candidate keys.

@@ -18,6 +18,8 @@ from .gridder_utils import (
 from .grid_wstack_wtower import (
     wstack_wtower_degrid_all,
     wstack_wtower_degrid_planes,
+    wstack_wtower_enable_timing,
+    wstack_wtower_get_timing,
     wstack_wtower_grid_all,
     wstack_wtower_grid_planes,
 )
@@ -42,6 +44,8 @@ __all__ = [
     "uvw_bounds_all",
     "wstack_wtower_degrid_all",
     "wstack_wtower_degrid_planes",
+    "wstack_wtower_enable_timing",
+    "wstack_wtower_get_timing",
     "wstack_wtower_grid_all",
     "wstack_wtower_grid_planes",
 ]

@@ -110,6 +110,24 @@ def wstack_wtower_grid_planes(vis, freq0_hz, dfreq_hz, uvw, subgrid_size,
     )
 
 
+def wstack_wtower_enable_timing(enable: bool = True):
+    """Switch HIP-event timing of the fused tower kernels on (resetting
+    the totals) or off."""
+    Lib.sdp_grid_wstack_wtower_enable_timing(int(enable))
+
+
+def wstack_wtower_get_timing():
+    """Totals since enable_timing(True): dict with kernel_ms, launches,
+    vis, layers, subgrid_size, kind ("grid" / "degrid"); None when off."""
+    out = (ctypes.c_double * 6)()
+    n = Lib.sdp_grid_wstack_wtower_get_timing(out, 6)
+    if n < 6:
+        return None
+    return {"kernel_ms": out[0], "launches": int(out[1]), "vis": int(out[2]),
+            "layers": int(out[3]), "subgrid_size": int(out[4]),
+            "kind": "degrid" if out[5] else "grid"}
+
+
 _M = Mem.handle_type()
 _I = ctypes.c_int
 _D = ctypes.c_double
@@ -121,3 +139,7 @@ for _name in ("degrid_all", "grid_all"):
 for _name in ("degrid_planes", "grid_planes"):
     Lib.wrap_func(f"sdp_grid_wstack_wtower_{_name}", restype=None,
                   argtypes=[_M] + _COMMON + [_I, _I], check_errcode=True)
+Lib.wrap_func("sdp_grid_wstack_wtower_enable_timing", restype=None,
+              argtypes=[_I])
+Lib.wrap_func("sdp_grid_wstack_wtower_get_timing", restype=_I,
+              argtypes=[ctypes.POINTER(_D), _I])
