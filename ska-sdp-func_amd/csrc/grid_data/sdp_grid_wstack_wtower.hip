@@ -561,16 +561,20 @@ __global__ void k_degrid_step(Cx<T>* __restrict__ wimg,
 // Degridding: cut the sub-grids out of the FFT'd grid
 // (sdp_gridder_subgrid_cut_out, utils.cpp:603-649) with the grid FFT's
 // output checkerboard and the sub-grid IFFT's input checkerboard; slots
-// [slots, slots_alloc) are zeroed.
+// [slots, slots_alloc) are zeroed. Grid: x = slot * nbx + column block,
+// y = sub-grid row, so no per-element division; the slot's grid offsets
+// (mod G) are uniform per block.
 template<typename T>
 __global__ void k_cut_out(const Cx<T>* __restrict__ grid, int64_t G,
         Cx<T>* __restrict__ wimg, int S, int64_t layer, const int* task,
         int64_t nv, int64_t min_iu, int64_t min_iv, int eff, int64_t slots,
-        int64_t n)
+        int nbx)
 {
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t slot = i / layer, e = i - slot * layer;
+    const int64_t slot = blockIdx.x / nbx;
+    const int b = (int)(blockIdx.x % nbx) * (int)blockDim.x + (int)threadIdx.x;
+    const int a = (int)blockIdx.y;
+    if (b >= S) return;
+    const int64_t i = slot * layer + (int64_t)a * S + b;
     if (slot >= slots)
     {
         wimg[i] = cx<T>(0, 0);
@@ -578,62 +582,79 @@ __global__ void k_cut_out(const Cx<T>* __restrict__ grid, int64_t G,
     }
     const int t = task[slot];
     const int64_t iu = min_iu + t / nv, iv = min_iv + t % nv;
-    const int64_t a = e / S, b = e % S;
-    int64_t gu = (a + G / 2 - S / 2 + iu * eff) % G;
-    int64_t gv = (b + G / 2 - S / 2 + iv * eff) % G;
-    if (gu < 0) gu += G;
-    if (gv < 0) gv += G;
+    int64_t ou = (G / 2 - S / 2 + iu * eff) % G;
+    int64_t ov = (G / 2 - S / 2 + iv * eff) % G;
+    if (ou < 0) ou += G;
+    if (ov < 0) ov += G;
+    int64_t gu = ou + a, gv = ov + b;      // a, b < S <= G
+    if (gu >= G) gu -= G;
+    if (gv >= G) gv -= G;
     const Cx<T> x = grid[gu * G + gv];
-    const bool neg = parity_sign(gu + gv + a + b) < 0;
+    const bool neg = ((gu + gv + a + b) & 1) != 0;
     wimg[i] = cx<T>(neg ? -x.re : x.re, neg ? -x.im : x.im);
 }
 
-__device__ __forceinline__ int64_t floor_div(int64_t a, int64_t b)
+// floor(x / d) for d > 0 and |x| < 2^24: a float estimate, corrected once.
+__device__ __forceinline__ int floor_div_small(int x, int d, float inv_d)
 {
-    return a >= 0 ? a / b : -((-a + b - 1) / b);
+    int q = (int)floorf((float)x * inv_d);
+    const int r = x - q * d;
+    if (r < 0) --q;
+    else if (r >= d) ++q;
+    return q;
 }
 
 // Gridding: grid (+)= sum of the FFT'd sub-grids covering each cell, in
 // the reference's task order (sdp_gridder_subgrid_add, utils.cpp:553-601,
 // sequential over tasks), with the sub-grid FFT's output checkerboard, the
-// grid IFFT's input checkerboard, and factor (image_size / S)^2.
+// grid IFFT's input checkerboard, and factor (image_size / S)^2. One block
+// row per grid row (the sub-grid rows covering it are uniform per block);
+// 32-bit index arithmetic (the host checks G < 2^22).
 template<typename T>
-__global__ void k_gather_grid(Cx<T>* __restrict__ grid, int64_t G,
+__global__ void k_gather_grid(Cx<T>* __restrict__ grid, int64_t G64,
         const Cx<T>* __restrict__ stack, int S,
-        const int* __restrict__ slot_of, int64_t nu, int64_t nv,
-        int64_t min_iu, int64_t min_iv, int eff, T factor, int accumulate)
+        const int* __restrict__ slot_of, int64_t nu64, int64_t nv64,
+        int64_t min_iu64, int64_t min_iv64, int eff, T factor, int accumulate)
 {
 #pragma clang fp contract(off)
-    const int64_t gv = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t gu = blockIdx.y;
+    const int G = (int)G64, nu = (int)nu64, nv = (int)nv64;
+    const int min_iu = (int)min_iu64, min_iv = (int)min_iv64;
+    const int gv = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int gu = (int)blockIdx.y;
     if (gv >= G) return;
-    Cx<T> acc = accumulate ? grid[gu * G + gv] : cx<T>(0, 0);
-    const bool neg_g = parity_sign(gu + gv) < 0;
-    const int64_t xu = gu - G / 2 + S / 2, xv = gv - G / 2 + S / 2;
+    const int64_t gi = (int64_t)gu * G + gv;
+    Cx<T> acc = accumulate ? grid[gi] : cx<T>(0, 0);
+    const bool neg_g = ((gu + gv) & 1) != 0;
+    const float inv_eff = 1.0f / (float)eff;
+    const int xu = gu - G / 2 + S / 2, xv = gv - G / 2 + S / 2;
+    const int64_t SS = (int64_t)S * S;
     for (int ku = -1; ku <= 1; ++ku)
     {
         // Sub-grids iu with 0 <= x - iu eff < S.
-        const int64_t x = xu + ku * G;
-        const int64_t iu_lo = max(floor_div(x - S + eff, eff), min_iu);
-        const int64_t iu_hi = min(floor_div(x, eff), min_iu + nu - 1);
-        for (int64_t iu = iu_lo; iu <= iu_hi; ++iu)
+        const int x = xu + ku * G;
+        const int iu_lo = max(floor_div_small(x - S + eff, eff, inv_eff),
+                min_iu);
+        const int iu_hi = min(floor_div_small(x, eff, inv_eff),
+                min_iu + nu - 1);
+        for (int iu = iu_lo; iu <= iu_hi; ++iu)
         {
-            const int64_t a = x - iu * eff;
+            const int a = x - iu * eff;
             if (a < 0 || a >= S) continue;
             for (int kv = -1; kv <= 1; ++kv)
             {
-                const int64_t y = xv + kv * G;
-                const int64_t iv_lo = max(floor_div(y - S + eff, eff),
-                        min_iv);
-                const int64_t iv_hi = min(floor_div(y, eff), min_iv + nv - 1);
-                for (int64_t iv = iv_lo; iv <= iv_hi; ++iv)
+                const int y = xv + kv * G;
+                const int iv_lo = max(floor_div_small(y - S + eff, eff,
+                        inv_eff), min_iv);
+                const int iv_hi = min(floor_div_small(y, eff, inv_eff),
+                        min_iv + nv - 1);
+                for (int iv = iv_lo; iv <= iv_hi; ++iv)
                 {
-                    const int64_t b = y - iv * eff;
+                    const int b = y - iv * eff;
                     if (b < 0 || b >= S) continue;
                     const int s = slot_of[(iu - min_iu) * nv + (iv - min_iv)];
                     if (s < 0) continue;
-                    const Cx<T> x0 = stack[(int64_t)s * S * S + a * S + b];
-                    const bool neg = parity_sign(a + b) < 0;
+                    const Cx<T> x0 = stack[s * SS + a * S + b];
+                    const bool neg = ((a + b) & 1) != 0;
                     T re = (neg ? -x0.re : x0.re) * factor;
                     T im = (neg ? -x0.im : x0.im) * factor;
                     if (neg_g)
@@ -647,7 +668,7 @@ __global__ void k_gather_grid(Cx<T>* __restrict__ grid, int64_t G,
             }
         }
     }
-    grid[gu * G + gv] = acc;
+    grid[gi] = acc;
 }
 
 // Gridding, image side of a w-stack plane: image += grid_correct(
@@ -2227,11 +2248,13 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
         if (*status) break;
         TowerParams p = tower_params(k, g, gr, b);
         const int64_t n_el = gr.slots * layer;
-        const int64_t n_alloc = gr.slots_alloc * layer;
         const int64_t ls = p.layer_stride;
-        k_cut_out<T><<<blocks_of(n_alloc), 256>>>(d_grid, G, d_wimg, g.S,
-                layer, p.task, g.nv, g.min_iu, g.min_iv, g.eff, gr.slots,
-                n_alloc);
+        {
+            const int nbx = (g.S + 255) / 256;
+            k_cut_out<T><<<dim3((unsigned)(gr.slots_alloc * nbx),
+                    (unsigned)g.S), 256>>>(d_grid, G, d_wimg, g.S, layer,
+                    p.task, g.nv, g.min_iu, g.min_iv, g.eff, gr.slots, nbx);
+        }
         sdp_fft::exec_2d(sp, d_wimg, false, 0, status);
         const int64_t first = gr.first_p + g.P0 - p.off_w;
         const int64_t last = gr.last_p + g.P0 - p.off_w;
@@ -2382,9 +2405,13 @@ bool check_args(const sdp_Mem* vis, const sdp_Mem* uvw, const sdp_Mem* image,
         return false;
     }
     if (sdp_mem_shape_dim(vis, 0) > 0x7FFFFFFF ||
-            sdp_mem_shape_dim(vis, 1) > 0x7FFFFFFF)
+            sdp_mem_shape_dim(vis, 1) > 0x7FFFFFFF ||
+            sdp_mem_shape_dim(image, 0) >= (1 << 22))
     {
+        // 32-bit row / sub-grid index arithmetic in the grid kernels.
         *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Too many rows / channels, or image of 2^22 pixels "
+                "or more a side");
         return false;
     }
     const sdp_MemType tv = sdp_mem_type(vis), tu = sdp_mem_type(uvw);
