@@ -1424,15 +1424,18 @@ __global__ void k_dft_check(const int4* __restrict__ vrec, int64_t n,
         atomicOr(flag, 1);
 }
 
-// pswf_n table of a plan's facet (a geometric constant: every w-stack
-// plane's correction divides by the same pswf_n(n(l, m))).
-__global__ void k_pn_table(CorrParams cp, double* __restrict__ tab)
+// Per-pixel correction scale of a plan's facet, 1 / (pswf(l) pswf(m)
+// pswf_n(n)) -- a geometric constant: every w-stack plane's correction
+// multiplies by the same value, so the image-side kernels read it (4 bytes
+// per pixel for float facets) instead of evaluating the PSWFs per call.
+template<typename S>
+__global__ void k_scale_table(CorrParams cp, S* __restrict__ tab)
 {
     const int64_t im = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t il = blockIdx.y;
     const int N = cp.image_size;
     if (im >= N) return;
-    tab[il * N + im] = pn_value((int)il - N / 2, (int)im - N / 2, cp);
+    tab[il * N + im] = (S)pixel_scale((int)il - N / 2, (int)im - N / 2, cp);
 }
 
 // ---------------------------------------------------------------------------
@@ -1516,28 +1519,37 @@ sdp_GridderWtowerUVW* cached_kernel(int image_size, int S, double theta,
     return k;
 }
 
-// Correction parameters with the plan's cached pswf_n table (built on
-// first use; plans are cached for the process lifetime by cached_kernel).
+// Correction parameters with the plan's cached per-pixel scale table, f32
+// for float facets and f64 for double ones (built on first use; plans are
+// cached for the process lifetime by cached_kernel).
 CorrParams corr_params_tab(const sdp_GridderWtowerUVW* k, int w_offset,
-        bool inverse, sdp_Error* status)
+        bool inverse, bool f32, sdp_Error* status)
 {
-    static std::map<const void*, double*> tabs;
+    static std::map<std::pair<const void*, bool>, void*> tabs;
     CorrParams cp = corr_params(k, w_offset, inverse);
-    auto it = tabs.find(k);
+    const auto key = std::make_pair((const void*)k, f32);
+    auto it = tabs.find(key);
     if (it == tabs.end())
     {
         const int64_t N = k->image_size;
-        double* d = nullptr;
-        if (hipMalloc(&d, N * N * sizeof(double)) != hipSuccess)
+        void* d = nullptr;
+        if (hipMalloc(&d, N * N * (f32 ? sizeof(float) : sizeof(double))) !=
+                hipSuccess)
         {
             (void)hipGetLastError();
             return cp;    // no room: evaluate per pixel
         }
-        k_pn_table<<<dim3(blocks_of(N), (unsigned)N), 256>>>(cp, d);
+        if (f32)
+            k_scale_table<float><<<dim3(blocks_of(N), (unsigned)N), 256>>>(
+                    cp, (float*)d);
+        else
+            k_scale_table<double><<<dim3(blocks_of(N), (unsigned)N), 256>>>(
+                    cp, (double*)d);
         SDP_HIP_CHECK_LAUNCH(status);
-        it = tabs.emplace(k, d).first;
+        it = tabs.emplace(key, d).first;
     }
-    cp.pn_tab = it->second;
+    if (f32) cp.scale_f32 = (const float*)it->second;
+    else cp.scale_f64 = (const double*)it->second;
     return cp;
 }
 
@@ -2121,7 +2133,7 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
             const double ti = now_s();
             sdp_fft::exec_2d(big, d_grid, false, 0, status);
             const CorrParams cp = corr_params_tab(k, (int)(gr.iw * g.H), true,
-                    status);
+                    sizeof(T) == 4, status);
             k_image_update<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
                     d_grid, G, image, (T)(1.0 / ((double)G * G)), cp);
             SDP_HIP_CHECK_LAUNCH(status);
@@ -2222,7 +2234,7 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
         {
             const double ti = now_s();
             const CorrParams cp = corr_params_tab(k, (int)(gr.iw * g.H),
-                    false, status);
+                    false, sizeof(T) == 4, status);
             k_image_to_grid<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
                     image, G, d_grid, cp);
             SDP_HIP_CHECK_LAUNCH(status);

@@ -633,6 +633,8 @@ CorrParams corr_params(const sdp_GridderWtowerUVW* plan, int w_offset,
     cp.w_offset = w_offset;
     cp.inverse = inverse ? 1 : 0;
     cp.pn_tab = nullptr;
+    cp.scale_f64 = nullptr;
+    cp.scale_f32 = nullptr;
     return cp;
 }
 

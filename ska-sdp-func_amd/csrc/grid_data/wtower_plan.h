@@ -59,7 +59,17 @@ struct CorrParams
     int w_offset;
     int inverse;              // grid_correct (1) or degrid_correct (0)
     const double* pn_tab;     // optional [image_size^2] table of pn_value
+    // Optional [image_size^2] tables of the whole per-pixel scale
+    // 1 / (pswf(l) pswf(m) pswf_n(n)), a geometric constant of the plan:
+    // f64 for double facets, f32 (the value the f32 facets multiply by)
+    // for float facets. When set, pn_tab is not read.
+    const double* scale_f64;
+    const float* scale_f32;
 };
+
+// 1 / (pswf(l) pswf(m) pswf_n(n)) of pixel (pl, pm) inside the image.
+__device__ __forceinline__ double pixel_scale(int pl, int pm,
+        const CorrParams& cp);
 
 // pswf_n(|2 w_step n|) of pixel (pl, pm) (1 outside the PSWF's support).
 __device__ __forceinline__ double pn_value(int pl, int pm,
@@ -72,6 +82,19 @@ __device__ __forceinline__ double pn_value(int pl, int pm,
     const double n = lm_to_n_dev(l, m, cp.shear_u, cp.shear_v);
     const double n_x = fabs(n * 2.0 * cp.w_step);
     return (n_x < 1.0) ? pswf_eval(cp.pswf_n, cp.n_pswf_n, n_x) : 1.0;
+}
+
+__device__ __forceinline__ double pixel_scale(int pl, int pm,
+        const CorrParams& cp)
+{
+#pragma clang fp contract(off)
+    const int half = cp.image_size / 2;
+    const double p_l = cp.pswf_lm[pl + half];
+    const double p_m = cp.pswf_lm[pm + half];
+    const double p_n = cp.pn_tab ?
+            cp.pn_tab[(int64_t)(pl + half) * cp.image_size + (pm + half)] :
+            pn_value(pl, pm, cp);
+    return 1.0 / (p_l * p_m * p_n);
 }
 
 CorrParams corr_params(const sdp_GridderWtowerUVW* plan, int w_offset,
@@ -90,15 +113,10 @@ __device__ __forceinline__ Cx<double> correct_value(Cx<double> z, int kind,
     if (pl + half < 0 || pl + half >= cp.image_size || pm + half < 0 ||
             pm + half >= cp.image_size)
         return z;
-    const double l = pl * cp.theta / cp.image_size;
-    const double m = pm * cp.theta / cp.image_size;
-    const double p_l = cp.pswf_lm[pl + half];
-    const double p_m = cp.pswf_lm[pm + half];
-    const double n = lm_to_n_dev(l, m, cp.shear_u, cp.shear_v);
-    const double p_n = cp.pn_tab ?
-            cp.pn_tab[(int64_t)(pl + half) * cp.image_size + (pm + half)] :
-            pn_value(pl, pm, cp);
-    const double scale = 1.0 / (p_l * p_m * p_n);
+    const int64_t idx = (int64_t)(pl + half) * cp.image_size + (pm + half);
+    const double scale = cp.scale_f64 ? cp.scale_f64[idx] :
+            (cp.scale_f32 && (kind == 0 || kind == 2)) ?
+            (double)cp.scale_f32[idx] : pixel_scale(pl, pm, cp);
     if (kind <= 1)
     {
         z.re *= (kind == 0) ? (double)(float)scale : scale;
@@ -117,6 +135,9 @@ __device__ __forceinline__ Cx<double> correct_value(Cx<double> z, int kind,
     }
     if (cp.w_offset != 0)
     {
+        const double l = pl * cp.theta / cp.image_size;
+        const double m = pm * cp.theta / cp.image_size;
+        const double n = lm_to_n_dev(l, m, cp.shear_u, cp.shear_v);
         const double phase = 2.0 * M_PI * cp.w_step * n * cp.w_offset;
         Cx<double> w = cx<double>(cos(phase), sin(phase));
         if (!cp.inverse) w = cdiv(cx<double>(1.0, 0.0), w);
