@@ -784,16 +784,23 @@ struct DftParams
     float2* part;                   // degrid: [visibility][tile] partials
 };
 
-template<typename U>
-__global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
+// NB: 16 x 16 pixel blocks per wave along the columns. A workgroup owns a
+// 32 x (32 NB) pixel tile; with NB = 2 each wave's two blocks share the row
+// taps (A operand) and the per-layer window / Horner bookkeeping, and their
+// independent accumulation chains keep the matrix core busier.
+template<typename U, int NB>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_dft(
+        DftParams d,
         const U* __restrict__ uvws, const Cx<float>* __restrict__ vis)
 {
 #pragma clang fp contract(off)
+    constexpr int kCols = kDftTile * NB;             // tile columns
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     __shared__ float2 s_tw[kDftMaxS];               // e^{2 pi i k / S}
     __shared__ int s_start[kDftLayers + 1];
     __shared__ float2 s_aku[kDftCap][kDftTile];     // V KU(l), tile rows
-    __shared__ float2 s_kv[kDftCap][kDftTile];      // KV(m), tile columns
+    __shared__ float2 s_kv[kDftCap][kCols];         // KV(m), tile columns
     // w taps keyed by absolute w-layer: s_kw[rs][(P + j) % 16] = kw_j,
     // so the rank update reads kw at layer L without first reading P.
     __shared__ float s_kw[kDftCap][16];
@@ -805,9 +812,9 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
     const TowerParams& tp = d.tp;
     const int S = tp.S, ws = tp.w_support, W = tp.support;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int tiles = S / kDftTile;
-    const int L0 = (blockIdx.x / tiles) * kDftTile;
-    const int M0 = (blockIdx.x % tiles) * kDftTile;
+    const int tiles_v = S / kCols;
+    const int L0 = (blockIdx.x / tiles_v) * kDftTile;
+    const int M0 = (blockIdx.x % tiles_v) * kCols;
     const int slot = blockIdx.y;
     const int64_t gs = d.gslot_base + slot;
     const int s0 = d.seg_start[gs], s1 = d.seg_end[gs];
@@ -816,7 +823,7 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
     // C layout: rows 4 (lane >> 4) + r, column lane & 15.
     const int bl = (wave >> 1) * 16, bm = (wave & 1) * 16;
     const int i = lane & 15, kq = lane >> 4;
-    const int pm = M0 + bm + i;
+    const int pm = M0 + bm + i;       // column of block 0; block nb: + 32 nb
     // The recurrence wimg = wimg / D + M_L runs in f32 within blocks of
     // kDftBlock layers (acc32, 1 / D rounded to f32) and in f64 across
     // blocks (acc64 = acc64 / D^kDftBlock + acc32): the reference keeps
@@ -825,25 +832,34 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
     // The f32 block partial lives in the matrix-core accumulators: each
     // layer first scales it by 1 / D, then the layer's rank update is
     // accumulated onto it (no zeroing / read-back of a separate layer sum).
-    Cx<double> acc[4], dinv_k[4];
-    float2 dinv32[4];
-    f32x4 a_re = {0.0f, 0.0f, 0.0f, 0.0f};
-    f32x4 a_im = {0.0f, 0.0f, 0.0f, 0.0f};
+    Cx<double> acc[NB][4], dinv_k[NB][4];
+    float2 dinv32[NB][4];
+    f32x4 a_re[NB], a_im[NB];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int nb = 0; nb < NB; ++nb)
     {
-        const int64_t e = (int64_t)(L0 + bl + 4 * kq + r) * S + pm;
-        acc[r] = cx<double>(0.0, 0.0);
-        const Cx<double> di = d.wp_inv[e];
-        dinv32[r] = make_float2((float)di.re, (float)di.im);
-        dinv_k[r] = cpow_int(di, kDftBlock);
+        a_re[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        a_im[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+        {
+            const int64_t e = (int64_t)(L0 + bl + 4 * kq + r) * S + pm +
+                    kDftTile * nb;
+            acc[nb][r] = cx<double>(0.0, 0.0);
+            const Cx<double> di = d.wp_inv[e];
+            dinv32[nb][r] = make_float2((float)di.re, (float)di.im);
+            dinv_k[nb][r] = cpow_int(di, kDftBlock);
+        }
     }
     Cx<float>* out = d.out + (int64_t)slot * S * S;
     if (n <= 0)
     {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-            out[(int64_t)(L0 + bl + 4 * kq + r) * S + pm] = cx<float>(0, 0);
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                out[(int64_t)(L0 + bl + 4 * kq + r) * S + pm + kDftTile * nb] =
+                        cx<float>(0, 0);
         return;
     }
     for (int k = t; k < S; k += 256) s_tw[k] = d.tw[k];
@@ -879,13 +895,15 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
         const int hi = s_start[max(0, min(npl, L + 1 - P_first))];
         // wimg = wimg / D (f32 within the block), then + layer below.
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-        {
-            const float xr = a_re[r], xi = a_im[r];
-            const float2 q = dinv32[r];
-            a_re[r] = xr * q.x - xi * q.y;
-            a_im[r] = xr * q.y + xi * q.x;
-        }
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+            {
+                const float xr = a_re[nb][r], xi = a_im[nb][r];
+                const float2 q = dinv32[nb][r];
+                a_re[nb][r] = xr * q.x - xi * q.y;
+                a_im[nb][r] = xr * q.y + xi * q.x;
+            }
         for (int a = lo; a < hi; a += kDftCap)
         {
             const int b = min(hi, a + kDftCap);
@@ -941,10 +959,12 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                     }
                 }
                 lds_sync();
-                for (int o = t; o < cnt * 2 * kDftTile; o += 256)
+                constexpr int kPer = kDftTile + kCols;   // rows, columns
+                for (int o = t; o < cnt * kPer; o += 256)
                 {
-                    const int v = x + (int)((unsigned)o / (2 * kDftTile));
-                    const int rs = v & (kDftCap - 1), q = o & (2 * kDftTile - 1);
+                    const int v = x + (int)((unsigned)o / kPer);
+                    const int rs = v & (kDftCap - 1);
+                    const int q = (int)((unsigned)o % kPer);
                     const int iu0 = s_tap[rs][0];
                     float2 res = make_float2(0.0f, 0.0f);
                     if (iu0 >= 0)
@@ -993,51 +1013,61 @@ __global__ __launch_bounds__(256) void k_tower_dft(DftParams d,
                 const bool ok = v < b;
                 const int rs = (ok ? v : a) & (kDftCap - 1);
                 const float2 av = s_aku[rs][bl + i];
-                const float2 bv = s_kv[rs][bm + i];
                 const float kw = ok ? s_kw[rs][L & 15] : 0.0f;
                 const float ar = av.x * kw, ai = av.y * kw;
-                a_re = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.x, a_re,
-                        0, 0, 0);
-                a_re = __builtin_amdgcn_mfma_f32_16x16x4f32(-ai, bv.y, a_re,
-                        0, 0, 0);
-                a_im = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.y, a_im,
-                        0, 0, 0);
-                a_im = __builtin_amdgcn_mfma_f32_16x16x4f32(ai, bv.x, a_im,
-                        0, 0, 0);
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb)
+                {
+                    const float2 bv = s_kv[rs][bm + kDftTile * nb + i];
+                    a_re[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.x,
+                            a_re[nb], 0, 0, 0);
+                    a_re[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(-ai, bv.y,
+                            a_re[nb], 0, 0, 0);
+                    a_im[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.y,
+                            a_im[nb], 0, 0, 0);
+                    a_im[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ai, bv.x,
+                            a_im[nb], 0, 0, 0);
+                }
             }
         }
         if ((L - L_first + 1 + blk_off) % kDftBlock == 0)
         {
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+            for (int nb = 0; nb < NB; ++nb)
             {
-                Cx<double> z = cmul(acc[r], dinv_k[r]);
-                z.re += (double)a_re[r];
-                z.im += (double)a_im[r];
-                acc[r] = z;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                {
+                    Cx<double> z = cmul(acc[nb][r], dinv_k[nb][r]);
+                    z.re += (double)a_re[nb][r];
+                    z.im += (double)a_im[nb][r];
+                    acc[nb][r] = z;
+                }
+                a_re[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                a_im[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
             }
-            a_re = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            a_im = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         }
     }
     // End of tower: wimg * D^(L_last - w_support / 2) (.cpp:1102-1113),
     // with the checkerboard of the forward FFT that follows.
     const int e_final = L_last - ws / 2;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-    {
-        const int pl = L0 + bl + 4 * kq + r;
-        const int64_t e = (int64_t)pl * S + pm;
-        Cx<double> z = acc[r];
-        if (e_final != 0) z = cmul(z, cpow_int(d.wp[e], e_final));
-        float re = (float)z.re, im = (float)z.im;
-        if ((pl + pm) & 1)
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
         {
-            re = -re;
-            im = -im;
+            const int pl = L0 + bl + 4 * kq + r, pc = pm + kDftTile * nb;
+            const int64_t e = (int64_t)pl * S + pc;
+            Cx<double> z = acc[nb][r];
+            if (e_final != 0) z = cmul(z, cpow_int(d.wp[e], e_final));
+            float re = (float)z.re, im = (float)z.im;
+            if ((pl + pc) & 1)
+            {
+                re = -re;
+                im = -im;
+            }
+            out[e] = cx<float>(re, im);
         }
-        out[e] = cx<float>(re, im);
-    }
 }
 
 // Fused w-tower degridding for complex-float visibilities (k_tower_idft),
@@ -2057,10 +2087,17 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                 dp.uv_kernel = k->d_uv_kernel;
                 dp.w_kernel = k->d_w_kernel;
                 dp.tw = dd.tw;
-                const int tiles = (g.S / kDftTile) * (g.S / kDftTile);
+                // Two 16 x 16 blocks per wave where the sub-grid allows.
+                const bool two = g.S % (2 * kDftTile) == 0;
+                const int tiles = (g.S / kDftTile) *
+                        (g.S / (two ? 2 * kDftTile : kDftTile));
                 tower_timing().start();
-                k_tower_dft<U><<<dim3(tiles, (unsigned)gr.slots), 256>>>(dp,
-                        d_uvw, (const Cx<float>*)d_vis);
+                if (two)
+                    k_tower_dft<U, 2><<<dim3(tiles, (unsigned)gr.slots),
+                            256>>>(dp, d_uvw, (const Cx<float>*)d_vis);
+                else
+                    k_tower_dft<U, 1><<<dim3(tiles, (unsigned)gr.slots),
+                            256>>>(dp, d_uvw, (const Cx<float>*)d_vis);
                 SDP_HIP_CHECK_LAUNCH(status);
                 tower_timing().stop();
                 sdp_fft::exec_2d(sp, d_stack, true, 0, status);
