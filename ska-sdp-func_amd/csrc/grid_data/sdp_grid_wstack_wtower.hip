@@ -1085,11 +1085,16 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_dft(
 // conj(KU) on the lanes and accumulates kw-weighted partials per
 // visibility in LDS. Partials of a (visibility, tile) pair are added to a
 // scratch row owned by the workgroup; k_idft_reduce sums the rows.
-template<typename U>
-__global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
-        const U* __restrict__ uvws)
+// NB: 16 x 16 pixel blocks per wave along the columns (tile 32 x 32 NB);
+// with NB = 2 a wave's two blocks extend the contraction T = Y conj(KV) over
+// 32 columns before the one row contraction / partial update per chunk.
+template<typename U, int NB>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_idft(
+        DftParams d, const U* __restrict__ uvws)
 {
 #pragma clang fp contract(off)
+    constexpr int kCols = kDftTile * NB;             // tile columns
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     __shared__ float2 s_tw[kDftMaxS];
     __shared__ int s_start[kDftLayers + 1];
@@ -1097,7 +1102,7 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
     // visibility's row (two 16-byte LDS reads) and the 16 lanes of a
     // quarter-wave, on 16 different rows, then cover all 64 banks once.
     __shared__ float2 s_ku[kDftCap][kDftTile + 2];  // conj KU(l), tile rows
-    __shared__ float2 s_kv[kDftCap][kDftTile + 2];  // conj KV(m), tile cols
+    __shared__ float2 s_kv[kDftCap][kCols + 2];     // conj KV(m), tile cols
     __shared__ float s_kw[kDftCap][17];             // keyed by w-layer % 16
     __shared__ int s_tap[kDftCap][5];
     __shared__ int s_P[kDftCap];
@@ -1107,16 +1112,16 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
     const TowerParams& tp = d.tp;
     const int S = tp.S, ws = tp.w_support, W = tp.support;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int tiles = S / kDftTile;
+    const int tiles_v = S / kCols;
     const int tile = blockIdx.x;
-    const int L0 = (tile / tiles) * kDftTile;
-    const int M0 = (tile % tiles) * kDftTile;
+    const int L0 = (tile / tiles_v) * kDftTile;
+    const int M0 = (tile % tiles_v) * kCols;
     const int slot = blockIdx.y;
     const int64_t gs = d.gslot_base + slot;
     const int s0 = d.seg_start[gs], s1 = d.seg_end[gs];
     const int n = s1 - s0;
     if (n <= 0) return;
-    const int ntiles = tiles * tiles;
+    const int ntiles = (S / kDftTile) * tiles_v;
     const int bl = (wave >> 1) * 16, bm = (wave & 1) * 16;
     const int i = lane & 15, kq = lane >> 4;
     const int shift = (int)(d.P0 - tp.off_w);
@@ -1128,21 +1133,25 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
     // (MFMA kk takes its k = kq from column bm + 4 kq + kk; any bijection
     // of the 16 columns works as long as A and B share it, and this one
     // puts a lane's 4 B entries next to each other in LDS).
-    Cx<double> y64[4], dinv_k[4];
-    float2 y32[4], dinv32[4];
+    Cx<double> y64[NB][4], dinv_k[NB][4];
+    float2 y32[NB][4], dinv32[NB][4];
     const Cx<float>* X = d.in + (int64_t)slot * S * S;
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk)
-    {
-        const int64_t e = (int64_t)(L0 + bl + i) * S + (M0 + bm + 4 * kq + kk);
-        const Cx<float> x = X[e];
-        y64[kk] = cmul(cx<double>((double)x.re, (double)x.im),
-                cpow_int(d.wp[e], -(L_first - ws / 2)));
-        const Cx<double> di = d.wp_inv[e];
-        dinv32[kk] = make_float2((float)di.re, (float)di.im);
-        dinv_k[kk] = cpow_int(di, kDftBlock);
-        y32[kk] = make_float2((float)y64[kk].re, (float)y64[kk].im);
-    }
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+        {
+            const int64_t e = (int64_t)(L0 + bl + i) * S +
+                    (M0 + kDftTile * nb + bm + 4 * kq + kk);
+            const Cx<float> x = X[e];
+            y64[nb][kk] = cmul(cx<double>((double)x.re, (double)x.im),
+                    cpow_int(d.wp[e], -(L_first - ws / 2)));
+            const Cx<double> di = d.wp_inv[e];
+            dinv32[nb][kk] = make_float2((float)di.re, (float)di.im);
+            dinv_k[nb][kk] = cpow_int(di, kDftBlock);
+            y32[nb][kk] = make_float2((float)y64[nb][kk].re,
+                    (float)y64[nb][kk].im);
+        }
     for (int k = t; k < S; k += 256) s_tw[k] = d.tw[k];
     for (int k = t; k < 4 * kDftCap; k += 256)
         s_acc[k / kDftCap][k & (kDftCap - 1)] = make_float2(0.0f, 0.0f);
@@ -1247,10 +1256,12 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
                     }
                 }
                 lds_sync();
-                for (int o = t; o < cnt * 2 * kDftTile; o += 256)
+                constexpr int kPer = kDftTile + kCols;   // rows, columns
+                for (int o = t; o < cnt * kPer; o += 256)
                 {
-                    const int v = x + (int)((unsigned)o / (2 * kDftTile));
-                    const int rs = v & (kDftCap - 1), q = o & (2 * kDftTile - 1);
+                    const int v = x + (int)((unsigned)o / kPer);
+                    const int rs = v & (kDftCap - 1);
+                    const int q = (int)((unsigned)o % kPer);
                     const int iu0 = s_tap[rs][0];
                     float2 res = make_float2(0.0f, 0.0f);
                     if (iu0 >= 0)
@@ -1291,22 +1302,26 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
                 const int rs = (ok ? v : a) & (kDftCap - 1);
                 f32x4 t_re = {0.0f, 0.0f, 0.0f, 0.0f};
                 f32x4 t_im = {0.0f, 0.0f, 0.0f, 0.0f};
-                float2 bv[4];
 #pragma unroll
-                for (int kk = 0; kk < 4; ++kk)
-                    bv[kk] = s_kv[rs][bm + 4 * kq + kk];
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk)
+                for (int nb = 0; nb < NB; ++nb)
                 {
-                    const float yr = y32[kk].x, yi = y32[kk].y;
-                    t_re = __builtin_amdgcn_mfma_f32_16x16x4f32(yr, bv[kk].x,
-                            t_re, 0, 0, 0);
-                    t_re = __builtin_amdgcn_mfma_f32_16x16x4f32(-yi, bv[kk].y,
-                            t_re, 0, 0, 0);
-                    t_im = __builtin_amdgcn_mfma_f32_16x16x4f32(yr, bv[kk].y,
-                            t_im, 0, 0, 0);
-                    t_im = __builtin_amdgcn_mfma_f32_16x16x4f32(yi, bv[kk].x,
-                            t_im, 0, 0, 0);
+                    float2 bv[4];
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk)
+                        bv[kk] = s_kv[rs][kDftTile * nb + bm + 4 * kq + kk];
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk)
+                    {
+                        const float yr = y32[nb][kk].x, yi = y32[nb][kk].y;
+                        t_re = __builtin_amdgcn_mfma_f32_16x16x4f32(yr,
+                                bv[kk].x, t_re, 0, 0, 0);
+                        t_re = __builtin_amdgcn_mfma_f32_16x16x4f32(-yi,
+                                bv[kk].y, t_re, 0, 0, 0);
+                        t_im = __builtin_amdgcn_mfma_f32_16x16x4f32(yr,
+                                bv[kk].y, t_im, 0, 0, 0);
+                        t_im = __builtin_amdgcn_mfma_f32_16x16x4f32(yi,
+                                bv[kk].x, t_im, 0, 0, 0);
+                    }
                 }
                 // Rows 4 kq + r of T for visibility i: contract with conj KU.
                 float pr = 0.0f, pi = 0.0f;
@@ -1337,21 +1352,26 @@ __global__ __launch_bounds__(256) void k_tower_idft(DftParams d,
         if ((L + 1 - L_first) % kDftBlock == 0)
         {
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-            {
-                y64[kk] = cmul(y64[kk], dinv_k[kk]);
-                y32[kk] = make_float2((float)y64[kk].re, (float)y64[kk].im);
-            }
+            for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                {
+                    y64[nb][kk] = cmul(y64[nb][kk], dinv_k[nb][kk]);
+                    y32[nb][kk] = make_float2((float)y64[nb][kk].re,
+                            (float)y64[nb][kk].im);
+                }
         }
         else
         {
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-            {
-                const float2 yv = y32[kk], q = dinv32[kk];
-                y32[kk] = make_float2(yv.x * q.x - yv.y * q.y,
-                        yv.x * q.y + yv.y * q.x);
-            }
+            for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                {
+                    const float2 yv = y32[nb][kk], q = dinv32[nb][kk];
+                    y32[nb][kk] = make_float2(yv.x * q.x - yv.y * q.y,
+                            yv.x * q.y + yv.y * q.x);
+                }
         }
     }
     lds_sync();
@@ -2224,7 +2244,10 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
     bool any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b, status);
     if (*status) return;
     DftData dd;
-    const int ntiles = (g.S / kDftTile) * (g.S / kDftTile);
+    // Two 16 x 16 blocks per wave (32 x 64 tiles) where the sub-grid allows.
+    const bool two = g.S % (2 * kDftTile) == 0;
+    const int ntiles = (g.S / kDftTile) *
+            (g.S / (two ? 2 * kDftTile : kDftTile));
     float2* d_part = nullptr;
     if (b.g.fused && any && !b.groups.empty() && b.n_items > 0)
     {
@@ -2328,8 +2351,12 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
                 dp.in = (const Cx<float>*)d_wimg;
                 dp.part = d_part;
                 tower_timing().start();
-                k_tower_idft<U><<<dim3(ntiles, (unsigned)gr.slots), 256>>>(
-                        dp, d_uvw);
+                if (two)
+                    k_tower_idft<U, 2><<<dim3(ntiles, (unsigned)gr.slots),
+                            256>>>(dp, d_uvw);
+                else
+                    k_tower_idft<U, 1><<<dim3(ntiles, (unsigned)gr.slots),
+                            256>>>(dp, d_uvw);
                 SDP_HIP_CHECK_LAUNCH(status);
                 tower_timing().stop();
             }
