@@ -19,7 +19,9 @@ grids its own 10M rows (a row shard of the job) into a partial image, then
 the partial images are summed onto rank 0 with one RCCL reduce (default,
 --reduce image: 5440^2 f32 = 118 MB) or the per-GPU grids are reduced before
 a single FFT on rank 0 (--reduce grid: 8192^2 c64 = 512 MiB). The collective
-is inside the timed region.
+is inside the timed region; with the image reduce, step k's reduce runs on
+RCCL's stream while step k + 1 grids into a second image buffer (every
+reduce completes before the clock stops; --no-overlap serialises them).
 
 Roofline: the dominant hand-written kernel's algorithmic bytes per launch
 divided by its HIP-event duration (library timing on the launch stream).
@@ -53,6 +55,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=10_000_000)
     ap.add_argument("--no-degrid", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="multi-GPU: wait for each step's reduce before the "
+                         "next step (default: reduce of step k overlaps "
+                         "step k + 1)")
     return ap.parse_args()
 
 
@@ -191,16 +197,40 @@ def main():
 
     from ska_sdp_func.grid_data.distributed import grid_sharded
 
+    # Multi-GPU, image reduce: two image buffers, so the RCCL reduce of
+    # batch k (issued asynchronously, on RCCL's stream) overlaps the
+    # kernels of batch k + 1; a buffer's reduce is waited on before the
+    # buffer is reused, and every reduce before the timed region ends.
+    pipelined = (world > 1 and args.reduce == "image" and
+                 not args.no_overlap)
+    bufs = [dirty, torch.zeros_like(dirty)] if pipelined else [dirty]
+    pending = [None] * len(bufs)
+    counter = [0]
+
     def grid_step():
+        k = counter[0] % len(bufs)
+        counter[0] += 1
+        img = bufs[k]
+        if pending[k] is not None:
+            pending[k].wait()
+            pending[k] = None
         # Fresh image per step (the call accumulates into it).
-        dirty.zero_()
+        img.zero_()
         if world == 1:
-            plan.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
+            plan.grid_uvw_es_fft(uvw, freq, vis, weight, img)
+        elif pipelined:
+            pending[k] = grid_sharded(plan, uvw, freq, vis, weight, img,
+                                      dist, mode="image", dst=0,
+                                      async_op=True)
         else:
-            grid_sharded(plan, uvw, freq, vis, weight, dirty, dist,
+            grid_sharded(plan, uvw, freq, vis, weight, img, dist,
                          mode=args.reduce, dst=0, grid_buf=grid_buf)
 
     def barrier():
+        for k, w in enumerate(pending):
+            if w is not None:
+                w.wait()
+                pending[k] = None
         torch.cuda.synchronize(dev)
         if dist is not None:
             dist.barrier()

@@ -29,13 +29,19 @@ def shard_rows(num_rows, rank, world):
 
 
 def grid_sharded(gridder, uvw, freq, vis, weight, dirty, dist, mode="image",
-                 dst=0, group=None, grid_buf=None):
+                 dst=0, group=None, grid_buf=None, async_op=False):
     """Grid this rank's rows and combine all ranks onto rank dst.
 
     uvw / vis / weight are THIS rank's rows. On return rank dst holds the
     gridded image (accumulated onto its input dirty image); other ranks'
     dirty buffers are scratch. grid_buf: [G, G] complex buffer for
     mode="grid" (allocated by the caller, reused across calls).
+
+    async_op (mode="image" only): the reduce is issued asynchronously and
+    its work handle returned instead of dirty; the caller waits on it
+    before reading dirty on rank dst or reusing the buffer, and can grid
+    the next batch into another buffer meanwhile (the collective then
+    overlaps the next batch's kernels).
 
     dst is a GLOBAL rank, as in torch.distributed.reduce, also when a
     group is given (it must then be a member of the group); the
@@ -51,8 +57,10 @@ def grid_sharded(gridder, uvw, freq, vis, weight, dirty, dist, mode="image",
         if rank != dst:
             dirty.zero_()
         gridder.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
-        dist.reduce(dirty, dst=dst, group=group)
-        return dirty
+        work = dist.reduce(dirty, dst=dst, group=group, async_op=async_op)
+        return work if async_op else dirty
+    if async_op:
+        raise ValueError("async_op needs mode='image'")
     if mode == "grid":
         if grid_buf is None:
             raise ValueError("mode='grid' needs grid_buf")
