@@ -758,6 +758,20 @@ __device__ __forceinline__ void lds_sync()
 // in an LDS ring (their tap sums over the tile's 32 rows and 32 columns,
 // in f32 like the reference's complex-float layers); the per-layer window
 // comes from an LDS table of layer starts.
+// D^e from the phase table, to f32 accuracy: the phase e * turns is reduced
+// to [-1/2, 1/2] turns in double and evaluated in single precision. Used
+// where the product is rounded to single precision anyway (end of a
+// gridding tower, start of a degridding one); binary powering in double
+// cost ~50 double operations and a 16-byte load per pixel.
+__device__ __forceinline__ Cx<double> pattern_pow_f32(double turns, int e)
+{
+    const double t = (double)e * turns;
+    const float f = (float)(t - rint(t));
+    float sn, cs;
+    sincospif(2.0f * f, &sn, &cs);
+    return cx<double>((double)cs, (double)sn);
+}
+
 constexpr int kDftCap = 32;      // staged visibilities (ring)
 constexpr int kDftTile = 32;     // tile edge (pixels)
 constexpr int kDftLayers = 512;  // max w-layers of a sub-grid's tower
@@ -777,6 +791,7 @@ struct DftParams
     Cx<float>* out;                 // [slots][S][S] (stack layer 0)
     const Cx<double>* wp;           // D
     const Cx<double>* wp_inv;       // 1 / D
+    const double* w_turns;          // D = exp(2 pi i w_turns)
     const double* uv_kernel;
     const double* w_kernel;
     const float2* tw;               // e^{2 pi i k / S}, k < S
@@ -1059,7 +1074,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_dft(
             const int pl = L0 + bl + 4 * kq + r, pc = pm + kDftTile * nb;
             const int64_t e = (int64_t)pl * S + pc;
             Cx<double> z = acc[nb][r];
-            if (e_final != 0) z = cmul(z, cpow_int(d.wp[e], e_final));
+            if (e_final != 0) z = cmul(z, pattern_pow_f32(d.w_turns[e], e_final));
             float re = (float)z.re, im = (float)z.im;
             if ((pl + pc) & 1)
             {
@@ -1145,7 +1160,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_idft(
                     (M0 + kDftTile * nb + bm + 4 * kq + kk);
             const Cx<float> x = X[e];
             y64[nb][kk] = cmul(cx<double>((double)x.re, (double)x.im),
-                    cpow_int(d.wp[e], -(L_first - ws / 2)));
+                    pattern_pow_f32(d.w_turns[e], -(L_first - ws / 2)));
             const Cx<double> di = d.wp_inv[e];
             dinv32[nb][kk] = make_float2((float)di.re, (float)di.im);
             dinv_k[nb][kk] = cpow_int(di, kDftBlock);
@@ -1415,6 +1430,21 @@ __global__ void k_pattern_inv(const Cx<double>* __restrict__ wp,
     if (i < n) inv[i] = cdiv(cx<double>(1.0, 0.0), wp[i]);
 }
 
+// Phase of the w-pattern in turns, w_step n(l, m) (D = exp(2 pi i turns),
+// sdp_gridder_utils.cpp:1353-1380; the host table's pixel geometry).
+__global__ void k_pattern_turns(double* __restrict__ turns, int S,
+        double theta, double shear_u, double shear_v, double w_step)
+{
+#pragma clang fp contract(off)
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= (int64_t)S * S) return;
+    const int il = (int)(i / S), im = (int)(i % S);
+    const double l = (il - S / 2) * theta / S;
+    const double m = (im - S / 2) * theta / S;
+    turns[i] = w_step * lm_to_n_dev(l, m, shear_u, shear_v);
+}
+
+
 // Expand sorted visibility runs (row, c0, c1, slot) into one record per
 // channel: (row, channel, w-layer relative to P0, group slot id).
 __global__ void k_expand_runs(const int4* __restrict__ items,
@@ -1520,7 +1550,7 @@ enum BufId
 {
     kRowCount, kRowOffset, kOccupied, kSlotMap, kKeys, kKeysAlt, kIdx,
     kIdxAlt, kItemsRaw, kItems, kHist, kTemp, kTasks, kSlotOf, kBounds,
-    kStack, kWimg, kGrid, kVrec, kSeg, kRunCnt, kRunOff, kWpInv, kFlag,
+    kStack, kWimg, kGrid, kVrec, kSeg, kRunCnt, kRunOff, kWpInv, kWTurns, kFlag,
     kGroupInfo, kTwiddle, kPart, kNumBuf
 };
 
@@ -1868,6 +1898,7 @@ struct DftData
     int* seg_start = nullptr;
     int* seg_end = nullptr;
     Cx<double>* wp_inv = nullptr;
+    double* w_turns = nullptr;
     float2* tw = nullptr;
     int64_t n_vis = 0;
 };
@@ -1910,6 +1941,8 @@ bool prepare_dft(const sdp_GridderWtowerUVW* k, const U* d_uvw,
     dd->seg_start = (int*)ws.get(kSeg, 2 * nseg * sizeof(int), status);
     dd->wp_inv = (Cx<double>*)ws.get(kWpInv,
             (size_t)g.S * g.S * sizeof(Cx<double>), status);
+    dd->w_turns = (double*)ws.get(kWTurns, (size_t)g.S * g.S * sizeof(double),
+            status);
     int* d_flag = (int*)ws.get(kFlag, sizeof(int), status);
     dd->tw = (float2*)ws.get(kTwiddle, g.S * sizeof(float2), status);
     int* d_ginfo = (int*)ws.get(kGroupInfo, 2 * ng * sizeof(int), status);
@@ -1927,6 +1960,8 @@ bool prepare_dft(const sdp_GridderWtowerUVW* k, const U* d_uvw,
     k_pattern_inv<<<blocks_of((int64_t)g.S * g.S), 256>>>(
             (const Cx<double>*)k->d_w_pattern, dd->wp_inv,
             (int64_t)g.S * g.S);
+    k_pattern_turns<<<blocks_of((int64_t)g.S * g.S), 256>>>(dd->w_turns,
+            g.S, k->theta, k->shear_u, k->shear_v, k->w_step);
     std::vector<int> ginfo(2 * ng);
     for (int64_t gi = 0; gi < ng; ++gi)
     {
@@ -2104,6 +2139,7 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                 dp.out = (Cx<float>*)d_stack;
                 dp.wp = wp;
                 dp.wp_inv = dd.wp_inv;
+                dp.w_turns = dd.w_turns;
                 dp.uv_kernel = k->d_uv_kernel;
                 dp.w_kernel = k->d_w_kernel;
                 dp.tw = dd.tw;
@@ -2345,6 +2381,7 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
                 dp.P0 = g.P0;
                 dp.wp = wp;
                 dp.wp_inv = dd.wp_inv;
+                dp.w_turns = dd.w_turns;
                 dp.uv_kernel = k->d_uv_kernel;
                 dp.w_kernel = k->d_w_kernel;
                 dp.tw = dd.tw;
