@@ -324,7 +324,13 @@ def main():
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
-                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+                pmc = json.load(f)
+            # Counters were collected at one workload: only reported for it.
+            wl = pmc.get("_workload", {})
+            if (wl.get("rows") == args.rows and wl.get("chan") == args.chan
+                    and wl.get("image") == args.image
+                    and wl.get("eps") == args.eps):
+                traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 
