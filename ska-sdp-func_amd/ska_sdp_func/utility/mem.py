@@ -71,6 +71,12 @@ class Mem(StructWrapper):
         elif torch is not None and isinstance(obj, torch.Tensor):
             mem_type = self._type_of(self._torch_dtype(obj.dtype), "torch")
             ptr = obj.data_ptr()
+            if ptr == 0 and obj.numel() == 0:
+                # torch reports NULL for empty views; pass the allocation's
+                # address (never dereferenced), as numpy does for empty
+                # arrays, so that the C side's type checks (which treat a
+                # NULL array as untyped, sdp_mem.cpp:643-647) see the dtype.
+                ptr = obj.untyped_storage().data_ptr()
             loc = (self.MemLocation.SDP_MEM_GPU if obj.is_cuda
                    else self.MemLocation.SDP_MEM_CPU)
             shape = tuple(obj.shape)

@@ -253,3 +253,40 @@ def test_scatter_grid_matches_oracle(device, rows):
     bad = np.argwhere(np.abs(out - ref) > 2e-6 * np.abs(ref).max())
     assert len(bad) == 0, (len(bad), bad[:5], out[tuple(bad[0])],
                            ref[tuple(bad[0])])
+
+
+@pytest.mark.parametrize("dbl", [False, True])
+def test_zero_rows(device, dbl):
+    """No visibility rows: gridding returns the corrected input image and
+    degridding corrects the image in place with nothing to write (the
+    reference's loops run zero times); no kernel may be launched with an
+    empty grid. The empty device arrays are views of allocated tensors:
+    like the reference (sdp_mem.cpp:643-647), a NULL data pointer makes an
+    array "not complex", which the argument checks reject."""
+    import torch
+    from ska_sdp_func.grid_data import GridderUvwEsFft
+
+    n = 128
+    uvw, freq, vis, wt, px = make_case(4, 500, 2, n, dbl=dbl)
+    rdt = np.float64 if dbl else np.float32
+    eps = 1e-12 if dbl else 1e-5
+    dirty0 = np.random.default_rng(8).standard_normal((n, n)).astype(rdt)
+    geo = es_oracle.geometry_for(uvw[:0], freq, vis[:0], dirty0, px, eps,
+                                 False)
+    g_uvw, g_vis, g_wt = (_gpu(a, device)[:0] for a in (uvw, vis, wt))
+    g_freq = _gpu(freq, device)
+    g_dirty = _gpu(dirty0, device)
+    plan = GridderUvwEsFft(g_uvw, g_freq, g_vis, g_wt, g_dirty, px, px, eps,
+                           False)
+    plan.grid_uvw_es_fft(g_uvw, g_freq, g_vis, g_wt, g_dirty)
+    ref = es_oracle.grid_uvw_es_fft(geo, uvw[:0], freq, vis[:0], wt[:0],
+                                    dirty0)
+    assert rel_l2(g_dirty.cpu().numpy(), ref) < TOL[dbl]
+    g_dirty = _gpu(dirty0, device)
+    plan.ifft_grid_uvw_es(g_uvw, g_freq, g_vis, g_wt, g_dirty)
+    torch.cuda.synchronize()
+    ref_vis, ref_dirty = es_oracle.ifft_degrid_uvw_es(geo, uvw[:0], freq,
+                                                      dirty0)
+    assert tuple(g_vis.shape) == ref_vis.shape == (0, 2)
+    assert rel_l2(g_dirty.cpu().numpy(), ref_dirty) < (1e-6 if not dbl
+                                                       else 1e-14)
