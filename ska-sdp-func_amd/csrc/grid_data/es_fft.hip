@@ -171,21 +171,27 @@ __device__ __forceinline__ void dft(float2* x)
 // (j / NS) * NS * R + j % NS + r * NS, after multiplying input r by
 // exp(SIGN 2 pi i r (j % NS) / (NS R)). First-stage inputs and last-stage
 // outputs are exchanged with the caller through load / store functors.
-template<int L, int P, int R0, int R1, int R2, int SIGN>
+template<int L, int P, int R0, int R1, int R2, int R3, int SIGN>
 struct Fft
 {
     static constexpr int EPT = L / P;
     static constexpr bool kThree = R2 > 1;
+    static constexpr bool kFour = R3 > 1;
+    static_assert(!kFour || kThree, "a fourth stage needs a third");
     static constexpr int NS1 = R0;
     static constexpr int NS2 = R0 * R1;
-    static constexpr int RL = kThree ? R2 : R1;
-    static_assert(R0 * R1 * (kThree ? R2 : 1) == L, "radices must multiply to L");
-    static_assert(EPT % R0 == 0 && EPT % R1 == 0 && (!kThree || EPT % R2 == 0),
+    static constexpr int NS3 = R0 * R1 * R2;
+    static constexpr int RL = kFour ? R3 : (kThree ? R2 : R1);
+    static_assert(R0 * R1 * (kThree ? R2 : 1) * (kFour ? R3 : 1) == L,
+            "radices must multiply to L");
+    static_assert(EPT % R0 == 0 && EPT % R1 == 0 && (!kThree || EPT % R2 == 0)
+            && (!kFour || EPT % R3 == 0),
             "each radix must divide the elements per thread");
     static_assert(R0 == 16, "first radix 16 (LDS layouts rely on it)");
     // Butterflies of one thread share the twiddles when P % NS == 0.
     static constexpr int TQ1 = (P % NS1 == 0) ? 1 : EPT / R1;
     static constexpr int TQ2 = kThree ? ((P % NS2 == 0) ? 1 : EPT / R2) : 1;
+    static constexpr int TQ3 = kFour ? ((P % NS3 == 0) ? 1 : EPT / R3) : 1;
 
     // Stage twiddles w^r (w = exp(SIGN 2 pi i k / (NS R)), r < R) are kept
     // as two short tables, w^b (b < LO) and w^(a LO) (a < R / LO), both read
@@ -205,6 +211,7 @@ struct Fft
     };
     StageTw<R1, TQ1> tw1;
     StageTw<kThree ? R2 : 2, TQ2> tw2;
+    StageTw<kFour ? R3 : 2, TQ3> tw3;
 
     // W[m] = exp(-2 pi i m / G); exp(SIGN 2 pi i a / b) = W^(a G / b)*.
     static __device__ __forceinline__ float2 twiddle(
@@ -238,6 +245,7 @@ struct Fft
     {
         init_stage<R1, NS1, TQ1>(tw1, p, W, G);
         if constexpr (kThree) init_stage<R2, NS2, TQ2>(tw2, p, W, G);
+        if constexpr (kFour) init_stage<R3, NS3, TQ3>(tw3, p, W, G);
     }
 
     // Called once per row / column block: makes the stored twiddles opaque
@@ -256,6 +264,7 @@ struct Fft
     {
         opaque_all(tw1);
         if constexpr (kThree) opaque_all(tw2);
+        if constexpr (kFour) opaque_all(tw3);
     }
 
     // v[0..R) *= w^r.
@@ -363,20 +372,37 @@ struct Fft
                 dft<SIGN, R2>(&v[q * R2]);
             }
         }
+        if constexpr (kFour)
+        {
+            exchange<R2, NS2, R3>(v, p, lds, idx);
+#pragma unroll
+            for (int q = 0; q < EPT / R3; ++q)
+            {
+                apply_stage<R3, TQ3>(&v[q * R3], tw3, q);
+                dft<SIGN, R3>(&v[q * R3]);
+            }
+        }
     }
 };
 
 // Row transform of length G: threads and radices.
 template<int G> struct RowPlan;
-template<> struct RowPlan<1024>  { static constexpr int P = 64,  R0 = 16, R1 = 16, R2 = 4; };
-template<> struct RowPlan<2048>  { static constexpr int P = 128, R0 = 16, R1 = 16, R2 = 8; };
-template<> struct RowPlan<4096>  { static constexpr int P = 256, R0 = 16, R1 = 16, R2 = 16; };
-template<> struct RowPlan<8192>  { static constexpr int P = 256, R0 = 16, R1 = 16, R2 = 32; };
-template<> struct RowPlan<16384> { static constexpr int P = 512, R0 = 16, R1 = 32, R2 = 32; };
+template<> struct RowPlan<1024>  { static constexpr int P = 64,  R0 = 16, R1 = 16, R2 = 4, R3 = 1; };
+template<> struct RowPlan<2048>  { static constexpr int P = 128, R0 = 16, R1 = 16, R2 = 8, R3 = 1; };
+template<> struct RowPlan<4096>  { static constexpr int P = 256, R0 = 16, R1 = 16, R2 = 16, R3 = 1; };
+#ifndef ES_ROW8K_P256
+// 512 threads, 16 elements each: half the registers of the 256-thread
+// three-stage plan, so the two workgroups an 8192-point row's LDS allows
+// per CU bring 4 waves per SIMD instead of 2.
+template<> struct RowPlan<8192>  { static constexpr int P = 512, R0 = 16, R1 = 8, R2 = 8, R3 = 8; };
+#else
+template<> struct RowPlan<8192>  { static constexpr int P = 256, R0 = 16, R1 = 16, R2 = 32, R3 = 1; };
+#endif
+template<> struct RowPlan<16384> { static constexpr int P = 512, R0 = 16, R1 = 32, R2 = 32, R3 = 1; };
 
 template<int G, int SIGN>
 using RowFft = Fft<G, RowPlan<G>::P, RowPlan<G>::R0, RowPlan<G>::R1,
-        RowPlan<G>::R2, SIGN>;
+        RowPlan<G>::R2, RowPlan<G>::R3, SIGN>;
 
 constexpr size_t row_lds_bytes(int G)
 {
@@ -392,7 +418,7 @@ struct ColPlan
 };
 
 template<int L, int SIGN>
-using ColFft = Fft<L, ColPlan<L>::P, 16, L / 16, 1, SIGN>;
+using ColFft = Fft<L, ColPlan<L>::P, 16, L / 16, 1, 1, SIGN>;
 
 constexpr size_t kColLdsBytes = 4096 * sizeof(float2);   // L * B = 4096
 
