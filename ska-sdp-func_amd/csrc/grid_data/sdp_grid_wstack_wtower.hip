@@ -772,6 +772,19 @@ __device__ __forceinline__ Cx<double> pattern_pow_f32(double turns, int e)
     return cx<double>((double)cs, (double)sn);
 }
 
+// Per-visibility staging record of the fused tower kernels, written once
+// per call by k_dft_prep instead of being rebuilt by every tile's
+// workgroup (which cost three dependent global round trips per staging
+// pass: record, uvw, kernel rows): words [0] iu0 (-1: invalid), [1] iv0,
+// [2] P (w-layer, tower numbering), [3] unused, [4, 6) V, then the W u taps
+// and W v taps (f32, zero if invalid), then 16 w taps keyed by absolute
+// w-layer, (P + j) % 16 (zeros elsewhere).
+constexpr int kPrepHdr = 6;
+__host__ __device__ constexpr int prep_stride(int W)
+{
+    return (kPrepHdr + 2 * W + 16 + 3) & ~3;
+}
+
 constexpr int kDftCap = 32;      // staged visibilities (ring)
 constexpr int kDftTile = 32;     // tile edge (pixels)
 constexpr int kDftLayers = 512;  // max w-layers of a sub-grid's tower
@@ -795,9 +808,36 @@ struct DftParams
     const double* uv_kernel;
     const double* w_kernel;
     const float2* tw;               // e^{2 pi i k / S}, k < S
+    const float* prep;              // per-visibility staging records
+    int prep_stride;                // words per record (prep_stride(W))
     const Cx<float>* in;            // degrid: [slots][S][S] sub-grid images
     float2* part;                   // degrid: [visibility][tile] partials
 };
+
+// Ring slots (x .. x + cnt) & (kDftCap - 1) <- records v0 .. v0 + cnt - 1.
+template<int KWN>
+__device__ __forceinline__ void stage_records(const DftParams& d, int64_t v0,
+        int x, int cnt, int W, int t, int (*s_tap)[2], float2* s_V,
+        float (*s_kuv)[32], float (*s_kw)[KWN])
+{
+    const int stride = d.prep_stride;
+    const float* src = d.prep + v0 * stride;
+    const int total = cnt * stride;
+    for (int o = t; o < total; o += 256)
+    {
+        const int vi = o / stride, w = o - vi * stride;
+        const int rs = (x + vi) & (kDftCap - 1);
+        const float f = src[o];
+        if (w < 2) s_tap[rs][w] = __float_as_int(f);
+        else if (w < 4) continue;
+        else if (w < kPrepHdr)
+        {
+            if (s_V) reinterpret_cast<float*>(&s_V[rs])[w - 4] = f;
+        }
+        else if (w < kPrepHdr + 2 * W) s_kuv[rs][w - kPrepHdr] = f;
+        else if (w < kPrepHdr + 2 * W + 16) s_kw[rs][w - kPrepHdr - 2 * W] = f;
+    }
+}
 
 // NB: 16 x 16 pixel blocks per wave along the columns. A workgroup owns a
 // 32 x (32 NB) pixel tile; with NB = 2 each wave's two blocks share the row
@@ -819,8 +859,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_dft(
     // w taps keyed by absolute w-layer: s_kw[rs][(P + j) % 16] = kw_j,
     // so the rank update reads kw at layer L without first reading P.
     __shared__ float s_kw[kDftCap][16];
-    __shared__ int s_tap[kDftCap][5];   // iu0 (-1: invalid), iv0, u/v/w offsets
-    __shared__ int s_P[kDftCap];
+    __shared__ int s_tap[kDftCap][2];   // iu0 (-1: invalid), iv0
     __shared__ float s_kuv[kDftCap][32];            // u taps, then v taps
     __shared__ float2 s_V[kDftCap];
 
@@ -894,9 +933,6 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_dft(
         const int pb = d.vrec[s0 + v].z + shift - P_first;
         for (int k = pa + 1; k <= pb; ++k) s_start[k] = v;
     }
-    const int task = tp.task[slot];
-    const int off_u = (int)((tp.min_iu + task / tp.nv) * tp.eff);
-    const int off_v = (int)((tp.min_iv + task % tp.nv) * tp.eff);
     int st_lo = 0, st_hi = 0;     // staged range (uniform)
     lds_sync();
 
@@ -934,45 +970,10 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_dft(
                 st_hi = e;
                 const int cnt = e - x;
                 lds_sync();   // ring slots free
-                if (t < cnt)
-                {
-                    const int v = x + t, rs = v & (kDftCap - 1);
-                    const int4 rec = d.vrec[s0 + v];
-                    TowerParams q = tp;
-                    q.w_plane = (int)(rec.z + d.P0 - tp.off_w);
-                    const Taps2 tt = item_taps(q, uvws, rec.x, rec.y, off_u,
-                            off_v);
-                    s_tap[rs][0] = tt.valid ? tt.iu0 : -1;
-                    s_tap[rs][1] = tt.iv0;
-                    s_tap[rs][2] = tt.u_off;
-                    s_tap[rs][3] = tt.v_off;
-                    s_tap[rs][4] = tt.w_off;
-                    s_P[rs] = q.w_plane;
-                    const Cx<float> vv = vis[(int64_t)rec.x * tp.num_chan +
-                            rec.y];
-                    s_V[rs] = make_float2(vv.re, vv.im);
-                }
-                lds_sync();
-                // Kernel rows of the staged visibilities: 2 W uv taps and
-                // w_support w taps each, one load per thread.
-                const int per = 2 * W + ws;
-                for (int o = t; o < cnt * per; o += 256)
-                {
-                    const int v = x + o / per, j = o % per;
-                    const int rs = v & (kDftCap - 1);
-                    const bool valid = s_tap[rs][0] >= 0;
-                    if (j < 2 * W)
-                    {
-                        const int koff = s_tap[rs][j < W ? 2 : 3] + j % W;
-                        s_kuv[rs][j] = valid ? (float)d.uv_kernel[koff] : 0.0f;
-                    }
-                    else
-                    {
-                        s_kw[rs][(s_P[rs] + j - 2 * W) & 15] = valid ?
-                                (float)d.w_kernel[s_tap[rs][4] + j - 2 * W] :
-                                0.0f;
-                    }
-                }
+                // Copy the staged visibilities' records (one dependent
+                // global load per word, 16-byte coalesced) into the ring.
+                stage_records(d, s0 + x, x, cnt, W, t, s_tap, s_V, s_kuv,
+                        s_kw);
                 lds_sync();
                 constexpr int kPer = kDftTile + kCols;   // rows, columns
                 for (int o = t; o < cnt * kPer; o += 256)
@@ -1119,8 +1120,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_idft(
     __shared__ float2 s_ku[kDftCap][kDftTile + 2];  // conj KU(l), tile rows
     __shared__ float2 s_kv[kDftCap][kCols + 2];     // conj KV(m), tile cols
     __shared__ float s_kw[kDftCap][17];             // keyed by w-layer % 16
-    __shared__ int s_tap[kDftCap][5];
-    __shared__ int s_P[kDftCap];
+    __shared__ int s_tap[kDftCap][2];
     __shared__ float s_kuv[kDftCap][32];
     __shared__ float2 s_acc[4][kDftCap];            // per-wave partials
 
@@ -1181,9 +1181,6 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_idft(
         const int pb = d.vrec[s0 + v].z + shift - P_first;
         for (int k = pa + 1; k <= pb; ++k) s_start[k] = v;
     }
-    const int task = tp.task[slot];
-    const int off_u = (int)((tp.min_iu + task / tp.nv) * tp.eff);
-    const int off_v = (int)((tp.min_iv + task % tp.nv) * tp.eff);
     int st_lo = 0, st_hi = 0;
     lds_sync();
 
@@ -1236,40 +1233,8 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? 3 : 1))) void k_tower_idft(
                 st_lo = a;
                 st_hi = e;
                 const int cnt = e - x;
-                if (t < cnt)
-                {
-                    const int v = x + t, rs = v & (kDftCap - 1);
-                    const int4 rec = d.vrec[s0 + v];
-                    TowerParams q = tp;
-                    q.w_plane = (int)(rec.z + d.P0 - tp.off_w);
-                    const Taps2 tt = item_taps(q, uvws, rec.x, rec.y, off_u,
-                            off_v);
-                    s_tap[rs][0] = tt.valid ? tt.iu0 : -1;
-                    s_tap[rs][1] = tt.iv0;
-                    s_tap[rs][2] = tt.u_off;
-                    s_tap[rs][3] = tt.v_off;
-                    s_tap[rs][4] = tt.w_off;
-                    s_P[rs] = q.w_plane;
-                }
-                lds_sync();
-                const int per = 2 * W + ws;
-                for (int o = t; o < cnt * per; o += 256)
-                {
-                    const int v = x + o / per, j = o % per;
-                    const int rs = v & (kDftCap - 1);
-                    const bool valid = s_tap[rs][0] >= 0;
-                    if (j < 2 * W)
-                    {
-                        const int koff = s_tap[rs][j < W ? 2 : 3] + j % W;
-                        s_kuv[rs][j] = valid ? (float)d.uv_kernel[koff] : 0.0f;
-                    }
-                    else
-                    {
-                        s_kw[rs][(s_P[rs] + j - 2 * W) & 15] = valid ?
-                                (float)d.w_kernel[s_tap[rs][4] + j - 2 * W] :
-                                0.0f;
-                    }
-                }
+                stage_records(d, s0 + x, x, cnt, W, t, s_tap, nullptr, s_kuv,
+                        s_kw);
                 lds_sync();
                 constexpr int kPer = kDftTile + kCols;   // rows, columns
                 for (int o = t; o < cnt * kPer; o += 256)
@@ -1490,14 +1455,17 @@ __global__ void k_segments(const int4* __restrict__ vrec, int64_t n,
     if (v == n - 1 || vrec[v + 1].w != gs) seg_end[gs] = (int)(v + 1);
 }
 
-// Flags visibilities whose uv taps leave the sub-grid: the reference wraps
-// them through its flat [w_support][S][S] stack indexing, which only the
+// Per-visibility staging records (see prep_stride), and a flag for
+// visibilities whose uv taps leave the sub-grid: the reference wraps them
+// through its flat [w_support][S][S] stack indexing, which only the
 // layer-by-layer path reproduces.
 template<typename U>
-__global__ void k_dft_check(const int4* __restrict__ vrec, int64_t n,
-        const U* __restrict__ uvws, TowerParams base,
-        const int* __restrict__ tasks, const int* __restrict__ g_offw,
-        const int* __restrict__ g_tbase, int64_t t_cap, int64_t P0,
+__global__ void k_dft_prep(const int4* __restrict__ vrec, int64_t n,
+        const U* __restrict__ uvws, const Cx<float>* __restrict__ vis,
+        TowerParams base, const int* __restrict__ tasks,
+        const int* __restrict__ g_offw, const int* __restrict__ g_tbase,
+        int64_t t_cap, int64_t P0, const double* __restrict__ uv_kernel,
+        const double* __restrict__ w_kernel, float* __restrict__ prep,
         int* __restrict__ flag)
 {
     const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -1514,6 +1482,33 @@ __global__ void k_dft_check(const int4* __restrict__ vrec, int64_t n,
     if (tt.valid && (tt.iu0 < 0 || tt.iu0 + q.support > q.S ||
             tt.iv0 < 0 || tt.iv0 + q.support > q.S))
         atomicOr(flag, 1);
+    const int W = q.support, ws = q.w_support;
+    float* r = prep + v * prep_stride(W);
+    r[0] = __int_as_float(tt.valid ? tt.iu0 : -1);
+    r[1] = __int_as_float(tt.iv0);
+    r[2] = __int_as_float(q.w_plane);
+    r[3] = 0.0f;
+    float vre = 0.0f, vim = 0.0f;
+    if (vis)
+    {
+        const Cx<float> vv = vis[(int64_t)rec.x * q.num_chan + rec.y];
+        vre = vv.re;
+        vim = vv.im;
+    }
+    r[4] = vre;
+    r[5] = vim;
+    for (int j = 0; j < W; ++j)
+    {
+        r[kPrepHdr + j] = tt.valid ? (float)uv_kernel[tt.u_off + j] : 0.0f;
+        r[kPrepHdr + W + j] = tt.valid ? (float)uv_kernel[tt.v_off + j] : 0.0f;
+    }
+    float kw[16];
+    for (int k = 0; k < 16; ++k) kw[k] = 0.0f;
+    for (int j = 0; j < ws; ++j)
+        kw[(q.w_plane + j) & 15] = tt.valid ? (float)w_kernel[tt.w_off + j] :
+                0.0f;
+    for (int k = 0; k < 16; ++k) r[kPrepHdr + 2 * W + k] = kw[k];
+    for (int k = kPrepHdr + 2 * W + 16; k < prep_stride(W); ++k) r[k] = 0.0f;
 }
 
 // Per-pixel correction scale of a plan's facet, 1 / (pswf(l) pswf(m)
@@ -1562,7 +1557,8 @@ enum BufId
 {
     kRowCount, kRowOffset, kOccupied, kSlotMap, kKeys, kKeysAlt, kIdx,
     kIdxAlt, kItemsRaw, kItems, kHist, kTemp, kTasks, kSlotOf, kBounds,
-    kStack, kWimg, kGrid, kVrec, kSeg, kRunCnt, kRunOff, kWpInv, kWTurns, kFlag,
+    kStack, kWimg, kGrid, kVrec, kSeg, kRunCnt, kRunOff, kWpInv, kWTurns,
+    kPrep, kFlag,
     kGroupInfo, kTwiddle, kPart, kNumBuf
 };
 
@@ -1911,6 +1907,8 @@ struct DftData
     int* seg_end = nullptr;
     Cx<double>* wp_inv = nullptr;
     double* w_turns = nullptr;
+    float* prep = nullptr;
+    int prep_stride = 0;
     float2* tw = nullptr;
     int64_t n_vis = 0;
 };
@@ -1920,7 +1918,8 @@ struct DftData
 // kDftLayers or a visibility's taps leave its sub-grid.
 template<typename U>
 bool prepare_dft(const sdp_GridderWtowerUVW* k, const U* d_uvw,
-        const Binned& b, DftData* dd, sdp_Error* status)
+        const Cx<float>* d_vis_in, const Binned& b, DftData* dd,
+        sdp_Error* status)
 {
     Workspace& ws = workspace();
     const Geo& g = b.g;
@@ -1955,6 +1954,9 @@ bool prepare_dft(const sdp_GridderWtowerUVW* k, const U* d_uvw,
             (size_t)g.S * g.S * sizeof(Cx<double>), status);
     dd->w_turns = (double*)ws.get(kWTurns, (size_t)g.S * g.S * sizeof(double),
             status);
+    dd->prep_stride = prep_stride(g.support);
+    dd->prep = (float*)ws.get(kPrep, (size_t)std::max<int64_t>(n_vis, 1) *
+            dd->prep_stride * sizeof(float), status);
     int* d_flag = (int*)ws.get(kFlag, sizeof(int), status);
     dd->tw = (float2*)ws.get(kTwiddle, g.S * sizeof(float2), status);
     int* d_ginfo = (int*)ws.get(kGroupInfo, 2 * ng * sizeof(int), status);
@@ -1986,9 +1988,9 @@ bool prepare_dft(const sdp_GridderWtowerUVW* k, const U* d_uvw,
     if (n_vis > 0)
     {
         const TowerParams base = tower_params(k, g, b.groups[0], b);
-        k_dft_check<U><<<blocks_of(n_vis), 256>>>(dd->vrec, n_vis, d_uvw,
-                base, b.d_tasks, d_ginfo, d_ginfo + ng, b.t_cap, g.P0,
-                d_flag);
+        k_dft_prep<U><<<blocks_of(n_vis), 256>>>(dd->vrec, n_vis, d_uvw,
+                d_vis_in, base, b.d_tasks, d_ginfo, d_ginfo + ng, b.t_cap,
+                g.P0, k->d_uv_kernel, k->d_w_kernel, dd->prep, d_flag);
     }
     SDP_HIP_CHECK_LAUNCH(status);
     int flag = 0;
@@ -2076,7 +2078,9 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
     if (*status) return;
     DftData dd;
     if (b.g.fused && any && !b.groups.empty() && b.n_items > 0 &&
-            !prepare_dft<U>(k, d_uvw, b, &dd, status))
+            !prepare_dft<U>(k, d_uvw, sizeof(T) == 4 ?
+                    (const Cx<float>*)(const void*)d_vis : nullptr, b, &dd,
+                    status))
     {
         if (*status) return;
         g.fused = 0;    // layer-by-layer path: re-bin in (layer, slot) order
@@ -2152,6 +2156,8 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                 dp.wp = wp;
                 dp.wp_inv = dd.wp_inv;
                 dp.w_turns = dd.w_turns;
+                dp.prep = dd.prep;
+                dp.prep_stride = dd.prep_stride;
                 dp.uv_kernel = k->d_uv_kernel;
                 dp.w_kernel = k->d_w_kernel;
                 dp.tw = dd.tw;
@@ -2299,7 +2305,7 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
     float2* d_part = nullptr;
     if (b.g.fused && any && !b.groups.empty() && b.n_items > 0)
     {
-        bool ok = prepare_dft<U>(k, d_uvw, b, &dd, status);
+        bool ok = prepare_dft<U>(k, d_uvw, nullptr, b, &dd, status);
         if (*status) return;
         const size_t part_bytes = (size_t)std::max<int64_t>(dd.n_vis, 1) *
                 ntiles * sizeof(float2);
@@ -2394,6 +2400,8 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
                 dp.wp = wp;
                 dp.wp_inv = dd.wp_inv;
                 dp.w_turns = dd.w_turns;
+                dp.prep = dd.prep;
+                dp.prep_stride = dd.prep_stride;
                 dp.uv_kernel = k->d_uv_kernel;
                 dp.w_kernel = k->d_w_kernel;
                 dp.tw = dd.tw;
