@@ -820,6 +820,7 @@ struct DftParams
     const float2* tw;               // e^{2 pi i k / S}, k < S
     const float* prep;              // per-visibility staging records
     int prep_stride;                // words per record (prep_stride(W))
+    float norm;                     // degrid: 1 / S^2 of the sub-grid IFFT
     const Cx<float>* in;            // degrid: [slots][S][S] sub-grid images
     float2* part;                   // degrid: [visibility][tile] partials
 };
@@ -1166,9 +1167,19 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk)
         {
-            const int64_t e = (int64_t)(L0 + bl + i) * S +
-                    (M0 + kDftTile * nb + bm + 4 * kq + kk);
-            const Cx<float> x = X[e];
+            const int pr = L0 + bl + i;
+            const int pc = M0 + kDftTile * nb + bm + 4 * kq + kk;
+            const int64_t e = (int64_t)pr * S + pc;
+            // Input checkerboard and 1 / S^2 of the sub-grid inverse FFT
+            // (.cpp:423-427), in single precision as the reference's layers.
+            Cx<float> x = X[e];
+            if ((pr + pc) & 1)
+            {
+                x.re = -x.re;
+                x.im = -x.im;
+            }
+            x.re *= d.norm;
+            x.im *= d.norm;
             y64[nb][kk] = cmul(cx<double>((double)x.re, (double)x.im),
                     pattern_pow_f32(d.w_turns[e], -(L_first - ws / 2)));
             const Cx<double> di = d.wp_inv[e];
@@ -2400,9 +2411,10 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
         {
             if constexpr (sizeof(T) == 4)
             {
-                k_degrid_init<T><<<blocks_of(n_el), 256>>>(d_wimg, wp, layer,
-                        g.S, norm, 0, n_el);
+                // The cut-out's checkerboard and 1 / S^2 are applied as
+                // k_tower_idft reads the sub-grid image (no separate pass).
                 DftParams dp = {};
+                dp.norm = (float)norm;
                 dp.tp = p;
                 dp.vrec = dd.vrec;
                 dp.seg_start = dd.seg_start;
