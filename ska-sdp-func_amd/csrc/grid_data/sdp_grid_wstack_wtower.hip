@@ -562,8 +562,12 @@ __global__ void k_degrid_step(Cx<T>* __restrict__ wimg,
 // (sdp_gridder_subgrid_cut_out, utils.cpp:603-649) with the grid FFT's
 // output checkerboard and the sub-grid IFFT's input checkerboard; slots
 // [slots, slots_alloc) are zeroed. Grid: x = slot * nbx + column block,
-// y = sub-grid row, so no per-element division; the slot's grid offsets
-// (mod G) are uniform per block.
+// y = block of kCutRows sub-grid rows (one per thread iteration, their loads
+// issued together: the kernel is bound by memory latency), so no
+// per-element division; the slot's grid offsets (mod G) are uniform per
+// block.
+constexpr int kCutRows = 4;
+
 template<typename T>
 __global__ void k_cut_out(const Cx<T>* __restrict__ grid, int64_t G,
         Cx<T>* __restrict__ wimg, int S, int64_t layer, const int* task,
@@ -572,12 +576,14 @@ __global__ void k_cut_out(const Cx<T>* __restrict__ grid, int64_t G,
 {
     const int64_t slot = blockIdx.x / nbx;
     const int b = (int)(blockIdx.x % nbx) * (int)blockDim.x + (int)threadIdx.x;
-    const int a = (int)blockIdx.y;
+    const int a0 = (int)blockIdx.y * kCutRows;
     if (b >= S) return;
-    const int64_t i = slot * layer + (int64_t)a * S + b;
+    Cx<T>* out = wimg + slot * layer + b;
     if (slot >= slots)
     {
-        wimg[i] = cx<T>(0, 0);
+#pragma unroll
+        for (int r = 0; r < kCutRows; ++r)
+            if (a0 + r < S) out[(int64_t)(a0 + r) * S] = cx<T>(0, 0);
         return;
     }
     const int t = task[slot];
@@ -586,12 +592,27 @@ __global__ void k_cut_out(const Cx<T>* __restrict__ grid, int64_t G,
     int64_t ov = (G / 2 - S / 2 + iv * eff) % G;
     if (ou < 0) ou += G;
     if (ov < 0) ov += G;
-    int64_t gu = ou + a, gv = ov + b;      // a, b < S <= G
-    if (gu >= G) gu -= G;
+    int64_t gv = ov + b;                  // b < S <= G
     if (gv >= G) gv -= G;
-    const Cx<T> x = grid[gu * G + gv];
-    const bool neg = ((gu + gv + a + b) & 1) != 0;
-    wimg[i] = cx<T>(neg ? -x.re : x.re, neg ? -x.im : x.im);
+    Cx<T> x[kCutRows];
+#pragma unroll
+    for (int r = 0; r < kCutRows; ++r)
+    {
+        int64_t gu = ou + a0 + r;
+        if (gu >= G) gu -= G;
+        x[r] = (a0 + r < S) ? grid[gu * G + gv] : cx<T>(0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < kCutRows; ++r)
+    {
+        const int a = a0 + r;
+        if (a >= S) break;
+        int64_t gu = ou + a;
+        if (gu >= G) gu -= G;
+        const bool neg = ((gu + gv + a + b) & 1) != 0;
+        out[(int64_t)a * S] = cx<T>(neg ? -x[r].re : x[r].re,
+                neg ? -x[r].im : x[r].im);
+    }
 }
 
 // floor(x / d) for d > 0 and |x| < 2^24: a float estimate, corrected once.
@@ -609,8 +630,13 @@ __device__ __forceinline__ int floor_div_small(int x, int d, float inv_d)
 // sequential over tasks), with the sub-grid FFT's output checkerboard, the
 // grid IFFT's input checkerboard, and factor (image_size / S)^2. One block
 // row per grid row (the sub-grid rows covering it are uniform per block);
-// 32-bit index arithmetic (the host checks G < 2^22).
-template<typename T>
+// 32-bit index arithmetic (the host checks G < 2^22). The candidate
+// sub-grids of a cell (at most kGatherCand per axis, host-checked) are
+// collected first, then all their slot lookups and then all their loads
+// are issued before the first is used: the kernel is bound by memory
+// latency, and a cell's 2-4 sub-grids were read one dependent pair of
+// loads at a time.
+template<typename T, int kGatherCand>
 __global__ void k_gather_grid(Cx<T>* __restrict__ grid, int64_t G64,
         const Cx<T>* __restrict__ stack, int S,
         const int* __restrict__ slot_of, int64_t nu64, int64_t nv64,
@@ -623,53 +649,74 @@ __global__ void k_gather_grid(Cx<T>* __restrict__ grid, int64_t G64,
     const int gu = (int)blockIdx.y;
     if (gv >= G) return;
     const int64_t gi = (int64_t)gu * G + gv;
-    Cx<T> acc = accumulate ? grid[gi] : cx<T>(0, 0);
-    const bool neg_g = ((gu + gv) & 1) != 0;
     const float inv_eff = 1.0f / (float)eff;
-    const int xu = gu - G / 2 + S / 2, xv = gv - G / 2 + S / 2;
-    const int64_t SS = (int64_t)S * S;
-    for (int ku = -1; ku <= 1; ++ku)
-    {
-        // Sub-grids iu with 0 <= x - iu eff < S.
-        const int x = xu + ku * G;
-        const int iu_lo = max(floor_div_small(x - S + eff, eff, inv_eff),
-                min_iu);
-        const int iu_hi = min(floor_div_small(x, eff, inv_eff),
-                min_iu + nu - 1);
-        for (int iu = iu_lo; iu <= iu_hi; ++iu)
+    // Candidates along one axis, ascending (wrap k = -1, 0, 1, then index).
+    auto candidates = [&](int x0, int lo_idx, int n_idx, int (&off)[kGatherCand],
+            int (&idx)[kGatherCand]) {
+        int nc = 0;
+        for (int k = -1; k <= 1; ++k)
         {
-            const int a = x - iu * eff;
-            if (a < 0 || a >= S) continue;
-            for (int kv = -1; kv <= 1; ++kv)
+            const int x = x0 + k * G;
+            const int i_lo = max(floor_div_small(x - S + eff, eff, inv_eff),
+                    lo_idx);
+            const int i_hi = min(floor_div_small(x, eff, inv_eff),
+                    lo_idx + n_idx - 1);
+            for (int ii = i_lo; ii <= i_hi; ++ii)
             {
-                const int y = xv + kv * G;
-                const int iv_lo = max(floor_div_small(y - S + eff, eff,
-                        inv_eff), min_iv);
-                const int iv_hi = min(floor_div_small(y, eff, inv_eff),
-                        min_iv + nv - 1);
-                for (int iv = iv_lo; iv <= iv_hi; ++iv)
-                {
-                    const int b = y - iv * eff;
-                    if (b < 0 || b >= S) continue;
-                    const int s = slot_of[(iu - min_iu) * nv + (iv - min_iv)];
-                    if (s < 0) continue;
-                    const Cx<T> x0 = stack[s * SS + a * S + b];
-                    const bool neg = ((a + b) & 1) != 0;
-                    T re = (neg ? -x0.re : x0.re) * factor;
-                    T im = (neg ? -x0.im : x0.im) * factor;
-                    if (neg_g)
-                    {
-                        re = -re;
-                        im = -im;
-                    }
-                    acc.re += re;
-                    acc.im += im;
-                }
+                const int o = x - ii * eff;
+                if (o < 0 || o >= S || nc >= kGatherCand) continue;
+                off[nc] = o;
+                idx[nc] = ii - lo_idx;
+                ++nc;
             }
         }
+        return nc;
+    };
+    int ua[kGatherCand], uu[kGatherCand], vb[kGatherCand], vv[kGatherCand];
+    const int nuc = candidates(gu - G / 2 + S / 2, min_iu, nu, ua, uu);
+    const int nvc = candidates(gv - G / 2 + S / 2, min_iv, nv, vb, vv);
+    constexpr int kC = kGatherCand * kGatherCand;
+    int slot[kC];
+#pragma unroll
+    for (int c = 0; c < kC; ++c)
+    {
+        const int cu = c / kGatherCand, cv = c % kGatherCand;
+        slot[c] = (cu < nuc && cv < nvc) ? slot_of[uu[cu] * nv + vv[cv]] : -1;
+    }
+    const int64_t SS = (int64_t)S * S;
+    Cx<T> x[kC];
+#pragma unroll
+    for (int c = 0; c < kC; ++c)
+    {
+        const int cu = c / kGatherCand, cv = c % kGatherCand;
+        x[c] = (slot[c] >= 0) ? stack[slot[c] * SS + ua[cu] * S + vb[cv]] :
+                cx<T>(0, 0);
+    }
+    Cx<T> acc = accumulate ? grid[gi] : cx<T>(0, 0);
+    const bool neg_g = ((gu + gv) & 1) != 0;
+#pragma unroll
+    for (int c = 0; c < kC; ++c)
+    {
+        if (slot[c] < 0) continue;
+        const int cu = c / kGatherCand, cv = c % kGatherCand;
+        const bool neg = ((ua[cu] + vb[cv]) & 1) != 0;
+        T re = (neg ? -x[c].re : x[c].re) * factor;
+        T im = (neg ? -x[c].im : x[c].im) * factor;
+        if (neg_g)
+        {
+            re = -re;
+            im = -im;
+        }
+        acc.re += re;
+        acc.im += im;
     }
     grid[gi] = acc;
 }
+
+// Image-side kernels: kImgRows grid rows per thread (blockIdx.y), all rows'
+// loads (grid / image values and correction scales) issued before the
+// arithmetic: these passes are bound by memory latency.
+constexpr int kImgRows = 4;
 
 // Gridding, image side of a w-stack plane: image += grid_correct(
 // checkerboard(IFFT(grid)) / G^2) (.cpp:702-711).
@@ -679,23 +726,47 @@ __global__ void k_image_update(const Cx<T>* __restrict__ grid, int64_t G,
 {
 #pragma clang fp contract(off)
     const int64_t gv = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t gu = blockIdx.y;
+    const int64_t gu0 = (int64_t)blockIdx.y * kImgRows;
     if (gv >= G) return;
-    const int64_t i = gu * G + gv;
-    Cx<T> x = grid[i];
-    if (parity_sign(gu + gv) < 0)
+    constexpr int kind = sizeof(T) == 8 ? 3 : 2;
+    const int pm = (int)(gv - G / 2);
+    Cx<T> x[kImgRows];
+    Cx<double> o[kImgRows];
+    double sc[kImgRows];
+#pragma unroll
+    for (int r = 0; r < kImgRows; ++r)
     {
-        x.re = -x.re;
-        x.im = -x.im;
+        const int64_t gu = gu0 + r;
+        const bool ok = gu < G;
+        const int64_t i = (ok ? gu : 0) * G + gv;
+        x[r] = grid[i];
+        o[r] = image.load(i);
+        const int pl = (int)(gu - G / 2);
+        sc[r] = (ok && corr_inside(pl, pm, cp)) ?
+                corr_scale(pl, pm, kind, cp) : 1.0;
     }
-    x.re *= norm;
-    x.im *= norm;
-    const Cx<double> z = correct_value(cx<double>(x.re, x.im),
-            sizeof(T) == 8 ? 3 : 2, (int)(gu - G / 2), (int)(gv - G / 2), cp);
-    Cx<double> o = image.load(i);
-    o.re += z.re;
-    if (image.kind >= 2) o.im += z.im;
-    image.store(i, o);
+#pragma unroll
+    for (int r = 0; r < kImgRows; ++r)
+    {
+        const int64_t gu = gu0 + r;
+        if (gu >= G) break;
+        Cx<T> v = x[r];
+        if (parity_sign(gu + gv) < 0)
+        {
+            v.re = -v.re;
+            v.im = -v.im;
+        }
+        v.re *= norm;
+        v.im *= norm;
+        const int pl = (int)(gu - G / 2);
+        Cx<double> z = cx<double>(v.re, v.im);
+        if (corr_inside(pl, pm, cp))
+            z = correct_scaled(z, kind, pl, pm, cp, sc[r]);
+        Cx<double> out = o[r];
+        out.re += z.re;
+        if (image.kind >= 2) out.im += z.im;
+        image.store(gu * G + gv, out);
+    }
 }
 
 // Degridding, image side of a w-stack plane: grid = checkerboard(
@@ -706,20 +777,39 @@ __global__ void k_image_to_grid(AnyView image, int64_t G,
 {
 #pragma clang fp contract(off)
     const int64_t gv = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t gu = blockIdx.y;
+    const int64_t gu0 = (int64_t)blockIdx.y * kImgRows;
     if (gv >= G) return;
-    const int64_t i = gu * G + gv;
-    const Cx<double> a = image.load(i);
-    const Cx<double> z = correct_value(cx<double>((double)(T)a.re,
-            (double)(T)a.im), sizeof(T) == 8 ? 3 : 2, (int)(gu - G / 2),
-            (int)(gv - G / 2), cp);
-    T re = (T)z.re, im = (T)z.im;
-    if (parity_sign(gu + gv) < 0)
+    constexpr int kind = sizeof(T) == 8 ? 3 : 2;
+    const int pm = (int)(gv - G / 2);
+    Cx<double> a[kImgRows];
+    double sc[kImgRows];
+#pragma unroll
+    for (int r = 0; r < kImgRows; ++r)
     {
-        re = -re;
-        im = -im;
+        const int64_t gu = gu0 + r;
+        const bool ok = gu < G;
+        a[r] = image.load((ok ? gu : 0) * G + gv);
+        const int pl = (int)(gu - G / 2);
+        sc[r] = (ok && corr_inside(pl, pm, cp)) ?
+                corr_scale(pl, pm, kind, cp) : 1.0;
     }
-    grid[i] = cx<T>(re, im);
+#pragma unroll
+    for (int r = 0; r < kImgRows; ++r)
+    {
+        const int64_t gu = gu0 + r;
+        if (gu >= G) break;
+        const int pl = (int)(gu - G / 2);
+        Cx<double> z = cx<double>((double)(T)a[r].re, (double)(T)a[r].im);
+        if (corr_inside(pl, pm, cp))
+            z = correct_scaled(z, kind, pl, pm, cp, sc[r]);
+        T re = (T)z.re, im = (T)z.im;
+        if (parity_sign(gu + gv) < 0)
+        {
+            re = -re;
+            im = -im;
+        }
+        grid[gu * G + gv] = cx<T>(re, im);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2253,9 +2343,26 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
             }
         }
         // Sub-grids into the grid.
-        k_gather_grid<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(d_grid, G,
-                d_stack, g.S, d_slot_of + gi * g.ntask, g.nu, g.nv, g.min_iu,
-                g.min_iv, g.eff, factor, gr.first_of_plane ? 0 : 1);
+        // Sub-grids covering a cell per axis: ceil(S / eff), plus one
+        // through the periodic wrap.
+        const int ncand = (g.S + g.eff - 1) / g.eff + 1;
+        if (ncand <= 3)
+            k_gather_grid<T, 3><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
+                    d_grid, G, d_stack, g.S, d_slot_of + gi * g.ntask, g.nu,
+                    g.nv, g.min_iu, g.min_iv, g.eff, factor,
+                    gr.first_of_plane ? 0 : 1);
+        else if (ncand <= 8)
+            k_gather_grid<T, 8><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
+                    d_grid, G, d_stack, g.S, d_slot_of + gi * g.ntask, g.nu,
+                    g.nv, g.min_iu, g.min_iv, g.eff, factor,
+                    gr.first_of_plane ? 0 : 1);
+        else
+        {
+            *status = SDP_ERR_INVALID_ARGUMENT;
+            SDP_LOG_ERROR("subgrid_frac too small: %d sub-grids overlap",
+                    ncand - 1);
+            break;
+        }
         SDP_HIP_CHECK_LAUNCH(status);
         if (verbosity > 0)
         {
@@ -2268,7 +2375,8 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
             sdp_fft::exec_2d(big, d_grid, false, 0, status);
             const CorrParams cp = corr_params_tab(k, (int)(gr.iw * g.H), true,
                     sizeof(T) == 4, status);
-            k_image_update<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
+            k_image_update<T><<<dim3(blocks_of(G),
+                    (unsigned)((G + kImgRows - 1) / kImgRows)), 256>>>(
                     d_grid, G, image, (T)(1.0 / ((double)G * G)), cp);
             SDP_HIP_CHECK_LAUNCH(status);
             if (verbosity > 0)
@@ -2372,7 +2480,8 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
             const double ti = now_s();
             const CorrParams cp = corr_params_tab(k, (int)(gr.iw * g.H),
                     false, sizeof(T) == 4, status);
-            k_image_to_grid<T><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
+            k_image_to_grid<T><<<dim3(blocks_of(G),
+                    (unsigned)((G + kImgRows - 1) / kImgRows)), 256>>>(
                     image, G, d_grid, cp);
             SDP_HIP_CHECK_LAUNCH(status);
             sdp_fft::exec_2d(big, d_grid, true, 0, status);
@@ -2401,7 +2510,7 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
         {
             const int nbx = (g.S + 255) / 256;
             k_cut_out<T><<<dim3((unsigned)(gr.slots_alloc * nbx),
-                    (unsigned)g.S), 256>>>(d_grid, G, d_wimg, g.S, layer,
+                    (unsigned)((g.S + kCutRows - 1) / kCutRows)), 256>>>(d_grid, G, d_wimg, g.S, layer,
                     p.task, g.nv, g.min_iu, g.min_iv, g.eff, gr.slots, nbx);
         }
         sdp_fft::exec_2d(sp, d_wimg, false, 0, status);

@@ -100,23 +100,33 @@ __device__ __forceinline__ double pixel_scale(int pl, int pm,
 CorrParams corr_params(const sdp_GridderWtowerUVW* plan, int w_offset,
         bool inverse);
 
-// Pixel (pl, pm) relative to the image centre of a facet of element kind
-// `kind` (AnyView): 1 / (pswf(l) pswf(m) pswf_n(n)), then, for complex
-// facets, the w-stacking phasor exp(+-2 pi i w_step n w_offset)
-// (sdp_gridder_grid_correct.cpp:18-116), in the facet's precision.
-// Pixels outside the image (undefined in the reference) are unchanged.
-__device__ __forceinline__ Cx<double> correct_value(Cx<double> z, int kind,
-        int pl, int pm, const CorrParams& cp)
+// Pixel (pl, pm) relative to the image centre inside the facet.
+__device__ __forceinline__ bool corr_inside(int pl, int pm,
+        const CorrParams& cp)
 {
-#pragma clang fp contract(off)
     const int half = cp.image_size / 2;
-    if (pl + half < 0 || pl + half >= cp.image_size || pm + half < 0 ||
-            pm + half >= cp.image_size)
-        return z;
+    return pl + half >= 0 && pl + half < cp.image_size && pm + half >= 0 &&
+            pm + half < cp.image_size;
+}
+
+// The pixel's 1 / (pswf(l) pswf(m) pswf_n(n)): from the plan's table when
+// there is one for the facet's precision, else evaluated.
+__device__ __forceinline__ double corr_scale(int pl, int pm, int kind,
+        const CorrParams& cp)
+{
+    const int half = cp.image_size / 2;
     const int64_t idx = (int64_t)(pl + half) * cp.image_size + (pm + half);
-    const double scale = cp.scale_f64 ? cp.scale_f64[idx] :
+    return cp.scale_f64 ? cp.scale_f64[idx] :
             (cp.scale_f32 && (kind == 0 || kind == 2)) ?
             (double)cp.scale_f32[idx] : pixel_scale(pl, pm, cp);
+}
+
+// correct_value with the pixel's scale already looked up (callers batch
+// the table loads of several pixels ahead of the arithmetic).
+__device__ __forceinline__ Cx<double> correct_scaled(Cx<double> z, int kind,
+        int pl, int pm, const CorrParams& cp, double scale)
+{
+#pragma clang fp contract(off)
     if (kind <= 1)
     {
         z.re *= (kind == 0) ? (double)(float)scale : scale;
@@ -138,8 +148,12 @@ __device__ __forceinline__ Cx<double> correct_value(Cx<double> z, int kind,
         const double l = pl * cp.theta / cp.image_size;
         const double m = pm * cp.theta / cp.image_size;
         const double n = lm_to_n_dev(l, m, cp.shear_u, cp.shear_v);
-        const double phase = 2.0 * M_PI * cp.w_step * n * cp.w_offset;
-        Cx<double> w = cx<double>(cos(phase), sin(phase));
+        // exp(2 pi i w_step n w_offset): the phase in turns is reduced to
+        // [-1/2, 1/2] in double before the (short-argument) sincospi.
+        const double turns = cp.w_step * n * cp.w_offset;
+        double sn, cs;
+        sincospi(2.0 * (turns - rint(turns)), &sn, &cs);
+        Cx<double> w = cx<double>(cs, sn);
         if (!cp.inverse) w = cdiv(cx<double>(1.0, 0.0), w);
         if (kind == 2)
         {
@@ -154,6 +168,18 @@ __device__ __forceinline__ Cx<double> correct_value(Cx<double> z, int kind,
         }
     }
     return z;
+}
+
+// Pixel (pl, pm) relative to the image centre of a facet of element kind
+// `kind` (AnyView): 1 / (pswf(l) pswf(m) pswf_n(n)), then, for complex
+// facets, the w-stacking phasor exp(+-2 pi i w_step n w_offset)
+// (sdp_gridder_grid_correct.cpp:18-116), in the facet's precision.
+// Pixels outside the image (undefined in the reference) are unchanged.
+__device__ __forceinline__ Cx<double> correct_value(Cx<double> z, int kind,
+        int pl, int pm, const CorrParams& cp)
+{
+    if (!corr_inside(pl, pm, cp)) return z;
+    return correct_scaled(z, kind, pl, pm, cp, corr_scale(pl, pm, kind, cp));
 }
 
 } // namespace sdp_wt
