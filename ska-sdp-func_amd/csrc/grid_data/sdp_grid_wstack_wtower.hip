@@ -1053,8 +1053,9 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
             {
                 const float xr = a_re[nb][r], xi = a_im[nb][r];
                 const float2 q = dinv32[nb][r];
-                a_re[nb][r] = xr * q.x - xi * q.y;
-                a_im[nb][r] = xr * q.y + xi * q.x;
+                // One rounding fewer than mul + add, and no pair packing.
+                a_re[nb][r] = __builtin_fmaf(xr, q.x, -(xi * q.y));
+                a_im[nb][r] = __builtin_fmaf(xr, q.y, xi * q.x);
             }
         for (int a = lo; a < hi; a += kDftCap)
         {
@@ -1472,8 +1473,9 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                 for (int kk = 0; kk < 4; ++kk)
                 {
                     const float2 yv = y32[nb][kk], q = dinv32[nb][kk];
-                    y32[nb][kk] = make_float2(yv.x * q.x - yv.y * q.y,
-                            yv.x * q.y + yv.y * q.x);
+                    y32[nb][kk] = make_float2(
+                            __builtin_fmaf(yv.x, q.x, -(yv.y * q.y)),
+                            __builtin_fmaf(yv.x, q.y, yv.y * q.x));
                 }
         }
     }
