@@ -89,3 +89,38 @@ def test_location_mismatch(device):
     flags = torch.zeros(vis.shape, dtype=torch.int32, device=device)
     with pytest.raises(CError, match="Error 6"):
         flagger_dynamic_threshold(vis, flags, **REF_ARGS)
+
+
+@pytest.mark.parametrize("dtype", [np.complex64, np.complex128])
+def test_threshold_boundaries(device, dtype):
+    """Magnitudes on the z-score threshold exactly and one unit in the last
+    place either side of it (integer magnitudes around median 12 with MAD 1
+    and threshold 0.6795 * 2, so z == thr for |m - 12| == 2), and a step
+    whose MAD is 0: the comparison shortcuts must decide these exactly as
+    the reference's double expression does."""
+    T, B, C = 6, 4, 64
+    rng = np.random.default_rng(11)
+    base = 12.0 + (np.arange(C) % 5) - 2.0          # 10 .. 14
+    vis = np.empty((T, B, C, 1), dtype)
+    real = np.float32 if dtype == np.complex64 else np.float64
+    for t in range(T):
+        for b in range(B):
+            m = base.astype(real).copy()
+            idx = rng.choice(C, 6, replace=False)
+            m[idx[0]] = np.nextafter(real(14.0), real(20.0))
+            m[idx[1]] = np.nextafter(real(14.0), real(0.0))
+            m[idx[2]] = np.nextafter(real(10.0), real(0.0))
+            m[idx[3]] = np.nextafter(real(10.0), real(20.0))
+            if t == 3:
+                m[:] = real(12.0)                    # MAD 0
+                m[idx[4]] = real(12.5)
+            vis[t, b, :, 0] = m.astype(dtype)
+    kw = dict(alpha=0.5, threshold_magnitudes=0.6795 * 2.0,
+              threshold_variations=1e6, threshold_broadband=1e6,
+              sampling_step=1, window=0, window_median_history=4)
+    flags = np.zeros(vis.shape, np.int32)
+    ref = fo.flagger_dynamic_threshold(vis, flags.copy(), **kw)
+    out = _gpu_flag(vis, flags, device, **kw)
+    assert ref.sum() > 0
+    assert np.array_equal(out, ref), (
+        f"{np.sum(out != ref)} of {ref.size} flags differ")
