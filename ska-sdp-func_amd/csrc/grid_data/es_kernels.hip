@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdlib>
 
+#include "utility/wave_ops.h"
 #include "es_kernels.h"
 #include "es_params.h"
 #include "es_image_dev.h"
@@ -1368,10 +1369,8 @@ __global__ __launch_bounds__(256) void k_gather_mfma(EsParams<float> p,
                     p_im += ku * t_im[rr];
                 }
                 // Sum the four lane groups (rows 4kq..4kq+3).
-                p_re += __shfl_xor(p_re, 16);
-                p_im += __shfl_xor(p_im, 16);
-                p_re += __shfl_xor(p_re, 32);
-                p_im += __shfl_xor(p_im, 32);
+                p_re = sdp_hip::sum_rows16(p_re);
+                p_im = sdp_hip::sum_rows16(p_im);
                 if (kq == 0 && valid)
                 {
                     const int e = __float_as_int(q.w);
@@ -1551,10 +1550,8 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
                     p_im += ku[rr] * t_im[rr];
                 }
                 // Sum the four lane groups (rows 4kq..4kq+3).
-                p_re += __shfl_xor(p_re, 16);
-                p_im += __shfl_xor(p_im, 16);
-                p_re += __shfl_xor(p_re, 32);
-                p_im += __shfl_xor(p_im, 32);
+                p_re = sdp_hip::sum_rows16(p_re);
+                p_im = sdp_hip::sum_rows16(p_im);
                 if (kq == 0 && valid)
                 {
                     const float kw = s_kw[e];

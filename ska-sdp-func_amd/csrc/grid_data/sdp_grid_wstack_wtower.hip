@@ -45,6 +45,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include "utility/wave_ops.h"
 #include "ska-sdp-func/grid_data/sdp_grid_wstack_wtower.h"
 #include "ska-sdp-func/grid_data/sdp_gridder_wtower_uvw.h"
 #include "wtower_dev.h"
@@ -1438,10 +1439,8 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                     pi = __builtin_fmaf(ku.x, t_im[r], pi);
                     pi = __builtin_fmaf(ku.y, t_re[r], pi);
                 }
-                pr += __shfl_xor(pr, 16);
-                pi += __shfl_xor(pi, 16);
-                pr += __shfl_xor(pr, 32);
-                pi += __shfl_xor(pi, 32);
+                pr = sdp_hip::sum_rows16(pr);
+                pi = sdp_hip::sum_rows16(pi);
                 if (kq == 0 && ok)
                 {
                     const float kw = s_kw[rs][L & 15];
