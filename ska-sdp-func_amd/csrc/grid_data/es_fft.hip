@@ -663,9 +663,21 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
             return ok ? gb.load(vo, so + e * (uint32_t)G * 8u)
                       : make_float2(0.f, 0.f);
         });
+        // The image values this thread adds to, loaded ahead of the
+        // transform: a load between two stores to the same image would
+        // wait for the store before it (possible alias), one round trip
+        // per element.
+        float prev[F::EPT];
+#pragma unroll
+        for (int i = 0; i < F::EPT; ++i)
+        {
+            const int iy = k2 + N2 * F::out_index(pq, i) - k0;
+            const bool in = ok && (unsigned)iy < (unsigned)M;
+            prev[i] = db.load_if(in, ((uint32_t)iy * ip.N + col) * 4u);
+        }
         f.transform(v, pq, lds, ColIdx<B>{cq});
         const float ccx = ip.conv_corr[min(abs(col - h), h)];
-        F::store_output(v, [&](int e, int, float2 x) {
+        F::store_output(v, [&](int e, int i, float2 x) {
             const int iy = k2 + N2 * (pq + e) - k0;
             const bool in = ok && (unsigned)iy < (unsigned)M;
             const int ix = col;
@@ -683,7 +695,7 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
                 val = x.x;
             }
             if ((ix + iy) & 1) val = -val;
-            float out = db.load_if(in, off) + val;
+            float out = prev[i] + val;
             if constexpr (!DO_W)
             {
                 // inv_correction (es_image_dev.h), 2-D branch, same order.
@@ -733,13 +745,23 @@ k_cols_a_image(float* __restrict__ dirty, int correct_in_place,
         const bool ok = col < M;
         float2 v[F::EPT];
         const float ccx = ip.conv_corr[min(abs(col - h), h)];
+        // All of the thread's image loads first, then the in-place
+        // correction stores: a load behind a store to the same image waits
+        // for it (possible alias), one round trip per element.
+        static_assert(F::EPT == 16, "one input slot per element (R0 = 16)");
+        F::load_input(v, [&](int e) {
+            const int iy = n1 + N1 * (pq + e) - k0;
+            const bool in = ok && (unsigned)iy < (unsigned)M;
+            return make_float2(db.load_if(in,
+                    ((uint32_t)iy * ip.N + col) * 4u), 0.0f);
+        });
         F::load_input(v, [&](int e) {
             const int iy = n1 + N1 * (pq + e) - k0;
             const bool in = ok && (unsigned)iy < (unsigned)M;
             const int ix = col;
             const int xo = ix - h, yo = iy - h;
             const uint32_t off = ((uint32_t)iy * ip.N + ix) * 4u;
-            float val = db.load_if(in, off);
+            float val = v[e / (N2 / 16)].x;
             if constexpr (!DO_W)
             {
                 // The 3-D path corrects the whole image before the planes.
@@ -898,10 +920,21 @@ int row_blocks(int G)
     return std::min(G, num_cus() * per_cu);
 }
 
+int col_wg_per_cu()
+{
+    static int v = 0;
+    if (!v)
+    {
+        const char* e = getenv("SDP_ES_COL_WG");
+        v = e ? std::max(1, atoi(e)) : 4;
+    }
+    return v;
+}
+
 dim3 col_grid(int fixed, int M, int B)
 {
     const int ncb = (M + B - 1) / B;
-    const int want = num_cus() * 4;
+    const int want = num_cus() * col_wg_per_cu();
     const int split = std::max(1, std::min(ncb, (want + fixed - 1) / fixed));
     return dim3(fixed, split);
 }

@@ -52,6 +52,10 @@ CASES = [
     (False, True, 1500, 2, 256, 1e-5),
     (True, True, 1500, 2, 256, 1e-10),
     (False, False, 20000, 1, 840, 0.05),   # config-1 kernel (G=1024, W=4)
+    # > 16 bucketing chunks of 8192 visibilities: every scan wave owns
+    # several chunk slots, walked XCD by XCD (k_scan_columns)
+    (False, False, 600000, 1, 256, 1e-5),
+    (False, True, 150000, 4, 256, 1e-5),
 ]
 
 
