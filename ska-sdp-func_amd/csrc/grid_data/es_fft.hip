@@ -920,13 +920,17 @@ int row_blocks(int G)
     return std::min(G, num_cus() * per_cu);
 }
 
+// Column-pass workgroups per CU (env SDP_ES_COL_WG for experiments). The
+// column kernels hold 3 workgroups per CU (VGPRs), so 6 per CU is two full
+// rounds; 4 left the second round two-thirds empty (config 2: grid FFT +
+// image 0.51 -> 0.48 ms, degrid 0.58 -> 0.53 ms with 6).
 int col_wg_per_cu()
 {
     static int v = 0;
     if (!v)
     {
         const char* e = getenv("SDP_ES_COL_WG");
-        v = e ? std::max(1, atoi(e)) : 4;
+        v = e ? std::max(1, atoi(e)) : 6;
     }
     return v;
 }
