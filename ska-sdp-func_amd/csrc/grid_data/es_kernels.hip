@@ -227,10 +227,30 @@ __global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = blockIdx.x * 64 + lane;
     const int per = (num_chunks + 15) / 16;
-    const int c0 = wave * per, c1 = min(num_chunks, c0 + per);
+    const int c0 = __builtin_amdgcn_readfirstlane(wave * per);
+    const int c1 = min(num_chunks, c0 + per);
+    // The wave's column of counts stays in registers between the two
+    // passes (the table is read once: 64 MiB at config 2).
+    constexpr int kMaxPer = kMaxChunks / 16;
+    static_assert(kMaxChunks % 16 == 0, "chunks split over 16 waves");
+    // Raw buffer view of the table: lane offset (bin) in one VGPR, chunk
+    // offset in an SGPR; lanes past nbins and chunks past c1 address out of
+    // range (loads return 0, stores are dropped).
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(table,
+            0, (int)((size_t)num_chunks * nbins * 4), 0x00020000);
+    const uint32_t voff = b < nbins ? (uint32_t)b * 4u : 0xFFFFFFF0u;
+    auto soff = [&](int k) -> uint32_t {
+        return c0 + k < c1 ? (uint32_t)((c0 + k) * nbins) * 4u : 0x7FFFFFF0u;
+    };
+    uint32_t val[kMaxPer];
     uint32_t sum = 0;
-    if (b < nbins)
-        for (int c = c0; c < c1; ++c) sum += table[(size_t)c * nbins + b];
+#pragma unroll
+    for (int k = 0; k < kMaxPer; ++k)
+    {
+        val[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, voff,
+                soff(k), 0);
+        sum += val[k];
+    }
     part[wave][lane] = sum;
     __syncthreads();
     if (wave == 0)
@@ -248,12 +268,11 @@ __global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
     if (b < nbins)
     {
         uint32_t run = part[wave][lane];
-        for (int c = c0; c < c1; ++c)
+#pragma unroll
+        for (int k = 0; k < kMaxPer; ++k)
         {
-            const size_t k = (size_t)c * nbins + b;
-            const uint32_t t = table[k];
-            table[k] = run;
-            run += t;
+            __builtin_amdgcn_raw_buffer_store_b32(run, rs, voff, soff(k), 0);
+            run += val[k];
         }
     }
 }
@@ -308,12 +327,21 @@ __global__ __launch_bounds__(1024) void k_scan_bins(
         uint32_t* __restrict__ totals, uint32_t* __restrict__ item_bin,
         uint32_t item_capacity)
 {
+    constexpr int kPer = 8;
+    constexpr int kRound = 1024 * kPer;
     __shared__ uint32_t s_a[32], s_b[32];
-    constexpr int kPer = 16;
+    // One output array of a round at a time, so that the global stores are
+    // coalesced (a thread owns kPer consecutive bins: storing them directly
+    // put every lane of a store instruction on its own line). Thread t's
+    // values at t * (kPer + 1) + k: the odd stride spreads a wave's LDS
+    // writes over all banks.
+    __shared__ uint32_t s_stage[1024 * (kPer + 1)];
+    auto slot = [](int i) { return (i / kPer) * (kPer + 1) + i % kPer; };
     const int t = threadIdx.x;
     uint32_t carry_c = 0, carry_i = 0;
-    for (int base = 0; base < nbins; base += 1024 * kPer)
+    for (int base = 0; base < nbins; base += kRound)
     {
+        const int nb = min(kRound, nbins - base);
         const int b0 = base + t * kPer;
         uint32_t n[kPer];
         if (b0 + kPer <= nbins)
@@ -342,19 +370,52 @@ __global__ __launch_bounds__(1024) void k_scan_bins(
         }
         uint32_t tot_c, tot_i;
         block_scan_1024(cnt, itm, s_a, s_b, tot_c, tot_i);
-        uint32_t run_c = carry_c + cnt, run_i = carry_i + itm;
+        // bin_start
+        uint32_t run = carry_c + cnt;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+        {
+            s_stage[t * (kPer + 1) + k] = run;
+            run += n[k];
+        }
+        __syncthreads();
+        for (int i = t; i < nb; i += 1024) bin_start[base + i] = s_stage[slot(i)];
+        __syncthreads();
+        // item_start
+        run = carry_i + itm;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k)
+        {
+            s_stage[t * (kPer + 1) + k] = run;
+            if (b0 + k < nbins) run += max(1u, (n[k] + kPiece - 1) / kPiece);
+        }
+        __syncthreads();
+        for (int i = t; i < nb; i += 1024) item_start[base + i] = s_stage[slot(i)];
+        __syncthreads();
+        // item -> bin: the round's first kRound items through LDS (linear),
+        // any further ones (bins split into many pieces) stored directly.
+        run = itm;   // item offset inside this round
+#pragma unroll
         for (int k = 0; k < kPer; ++k)
         {
             const int bb = b0 + k;
             if (bb >= nbins) break;
             const uint32_t ni = max(1u, (n[k] + kPiece - 1) / kPiece);
-            bin_start[bb] = run_c;
-            item_start[bb] = run_i;
             for (uint32_t j = 0; j < ni; ++j)
-                if (run_i + j < item_capacity) item_bin[run_i + j] = (uint32_t)bb;
-            run_c += n[k];
-            run_i += ni;
+            {
+                const uint32_t r = run + j;
+                if (r < (uint32_t)kRound)
+                    s_stage[slot((int)r)] = (uint32_t)bb;
+                else if (carry_i + r < item_capacity)
+                    item_bin[carry_i + r] = (uint32_t)bb;
+            }
+            run += ni;
         }
+        __syncthreads();
+        const int ni_lds = (int)min(tot_i, (uint32_t)kRound);
+        for (int i = t; i < ni_lds; i += 1024)
+            if (carry_i + i < item_capacity) item_bin[carry_i + i] = s_stage[slot(i)];
+        __syncthreads();
         carry_c += tot_c;
         carry_i += tot_i;
     }
