@@ -920,25 +920,37 @@ int row_blocks(int G)
     return std::min(G, num_cus() * per_cu);
 }
 
-// Column-pass workgroups per CU (env SDP_ES_COL_WG for experiments). The
-// column kernels hold 3 workgroups per CU (VGPRs), so 6 per CU is two full
-// rounds; 4 left the second round two-thirds empty (config 2: grid FFT +
-// image 0.51 -> 0.48 ms, degrid 0.58 -> 0.53 ms with 6).
-int col_wg_per_cu()
+// Column-pass workgroups: rounds x the kernel's resident workgroups per CU
+// (env SDP_ES_COL_ROUNDS for experiments; default 2). A launch that is not
+// a whole number of resident rounds leaves its last round partly empty:
+// 4 per CU for the kernels that hold 3 (VGPRs) cost config 2 0.03 ms of
+// grid FFT + image and 0.05 ms of degrid FFT; the degrid column pass B
+// holds 5 (LDS) and ran 1.2 rounds at 6 per CU.
+int col_rounds()
 {
     static int v = 0;
     if (!v)
     {
-        const char* e = getenv("SDP_ES_COL_WG");
-        v = e ? std::max(1, atoi(e)) : 6;
+        const char* e = getenv("SDP_ES_COL_ROUNDS");
+        v = e ? std::max(1, atoi(e)) : 2;
     }
     return v;
 }
 
+template<auto Kernel>
 dim3 col_grid(int fixed, int M, int B)
 {
+    static int occ = 0;
+    if (!occ)
+    {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, Kernel, 256,
+                kColLdsBytes) != hipSuccess || n <= 0)
+            n = 3;
+        occ = n;
+    }
     const int ncb = (M + B - 1) / B;
-    const int want = num_cus() * col_wg_per_cu();
+    const int want = num_cus() * occ * col_rounds();
     const int split = std::max(1, std::min(ncb, (want + fixed - 1) / fixed));
     return dim3(fixed, split);
 }
@@ -970,7 +982,8 @@ int grid_rows_cols(const Geometry& g, const float2* W, float2* grid,
             grid, g.k0, g.M, W, tiles, ncoarse);
     SDP_HIP_CHECK_LAUNCH(&st);
     if (st) return st;
-    k_cols_a_grid<N1, N2><<<col_grid(N1, g.M, ColPlan<N2>::B), 256,
+    k_cols_a_grid<N1, N2><<<col_grid<k_cols_a_grid<N1, N2>>(N1, g.M,
+            ColPlan<N2>::B), 256,
             kColLdsBytes, stream>>>(grid, g.M, W);
     SDP_HIP_CHECK_LAUNCH(&st);
     return st;
@@ -981,7 +994,9 @@ int grid_to_image(const Geometry& g, const ImageParams<float>& ip, int plane,
         const float2* W, const float2* grid, float* dirty, hipStream_t stream)
 {
     sdp_Error st = SDP_SUCCESS;
-    const dim3 blocks = col_grid(N2, g.M, ColPlan<N1>::B);
+    const dim3 blocks = ip.do_w ?
+            col_grid<k_cols_b_grid<N1, N2, true>>(N2, g.M, ColPlan<N1>::B) :
+            col_grid<k_cols_b_grid<N1, N2, false>>(N2, g.M, ColPlan<N1>::B);
     if (ip.do_w)
         k_cols_b_grid<N1, N2, true><<<blocks, 256, kColLdsBytes, stream>>>(
                 grid, dirty, ip, plane, g.k0, g.M, W);
@@ -998,7 +1013,9 @@ int image_cols(const Geometry& g, const ImageParams<float>& ip, int plane,
         hipStream_t stream)
 {
     sdp_Error st = SDP_SUCCESS;
-    const dim3 blocks = col_grid(N1, g.M, ColPlan<N2>::B);
+    const dim3 blocks = ip.do_w ?
+            col_grid<k_cols_a_image<N1, N2, true>>(N1, g.M, ColPlan<N2>::B) :
+            col_grid<k_cols_a_image<N1, N2, false>>(N1, g.M, ColPlan<N2>::B);
     if (ip.do_w)
         k_cols_a_image<N1, N2, true><<<blocks, 256, kColLdsBytes, stream>>>(
                 dirty, correct ? 1 : 0, grid, ip, plane, g.k0, g.M, W);
@@ -1015,7 +1032,8 @@ int image_to_grid(const Geometry& g, const float2* W, float2* grid,
 {
     constexpr int G = N1 * N2;
     sdp_Error st = SDP_SUCCESS;
-    k_cols_b_image<N1, N2><<<col_grid(N2, g.M, ColPlan<N1>::B), 256,
+    k_cols_b_image<N1, N2><<<col_grid<k_cols_b_image<N1, N2>>(N2, g.M,
+            ColPlan<N1>::B), 256,
             kColLdsBytes, stream>>>(grid, g.M, W);
     SDP_HIP_CHECK_LAUNCH(&st);
     if (st) return st;
