@@ -69,6 +69,21 @@ int fft_image_cols(const ImageParams<float>& ip, int plane,
 int fft_image_to_grid(const ImageParams<float>& ip, const FftTwiddles& tw,
         float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream);
 
+// Whole-grid 2-D FFT of a complex-float G x G grid in place, unnormalised
+// (forward e^-, inverse e^+, as rocFFT / cuFFT), in three passes (rows,
+// then the four-step columns). The result's row k is stored at row
+// fft_perm_row(k): callers read it through that permutation.
+int fft2d_inplace_permuted(float* grid, int grid_size, bool forward,
+        const FftTwiddles& tw, hipStream_t stream);
+// N2 of the column split (G = N1 * N2; 0 if the size is not supported).
+int fft_perm_n2(int grid_size);
+// Storage row of the transform's row k: N1 * (k % N2) + k / N2.
+__host__ __device__ __forceinline__ int64_t fft_perm_row(int64_t k,
+        int64_t G, int n2)
+{
+    return n2 ? (G / n2) * (k % n2) + k / n2 : k;
+}
+
 } // namespace sdp_es
 
 #endif

@@ -592,12 +592,12 @@ k_rows_grid(float2* __restrict__ grid, int k0, int M,
 
 // Column pass A (inverse): for u1 = blockIdx.x, length-N2 FFTs over rows
 // u1 + N1 * n2, times W^(u1 k2)*, back into rows u1 + N1 * k2.
-template<int N1, int N2>
+template<int N1, int N2, int SIGN = 1>
 __global__ void __launch_bounds__(256)
 k_cols_a_grid(float2* __restrict__ grid, int M, const float2* __restrict__ W)
 {
     constexpr int G = N1 * N2, B = ColPlan<N2>::B;
-    using F = ColFft<N2, 1>;
+    using F = ColFft<N2, SIGN>;
     extern __shared__ float2 lds[];
     const int c = threadIdx.x % B, p = threadIdx.x / B;
     const int u1 = blockIdx.x;
@@ -704,6 +704,42 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
                 out *= 1.0f / corr;
             }
             db.store_if(in, out, off);
+        });
+    }
+}
+
+// Column pass B in place (full 2-D FFTs of a whole grid, w-stacking): for
+// k2 = blockIdx.x, length-N1 FFTs over the contiguous rows N1 * k2 + n1,
+// output k1 back into row N1 * k2 + k1. Natural row k = k2 + N2 * k1 of the
+// transform is then stored at row N1 * (k % N2) + k / N2 (fft_perm_row).
+template<int N1, int N2, int SIGN>
+__global__ void __launch_bounds__(256)
+k_cols_b_block(float2* __restrict__ grid, int M, const float2* __restrict__ W)
+{
+    constexpr int G = N1 * N2, B = ColPlan<N1>::B;
+    using F = ColFft<N1, SIGN>;
+    extern __shared__ float2 lds[];
+    const int c = threadIdx.x % B, p = threadIdx.x / B;
+    const int k2 = blockIdx.x;
+    const Buf gb(grid, grid_bytes(G, 0));
+    F f;
+    f.init(p, W, G);
+    const int ncb = (M + B - 1) / B;
+    const uint32_t so = (uint32_t)N1 * k2 * G * 8u;
+    constexpr uint32_t kStep = (uint32_t)G * 8u;
+    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
+    {
+        const int pq = opaque(p), cq = opaque(c);
+        const int col = cb * B + cq;
+        const bool ok = col < M;
+        const uint32_t vo = ((uint32_t)pq * G + col) * 8u;
+        float2 v[F::EPT];
+        F::load_input(v, [&](int e) {
+            return ok ? gb.load(vo, so + e * kStep) : make_float2(0.f, 0.f);
+        });
+        f.transform(v, pq, lds, ColIdx<B>{cq});
+        F::store_output(v, [&](int e, int, float2 x) {
+            if (ok) gb.store(x, vo, so + e * kStep);
         });
     }
 }
@@ -1046,6 +1082,52 @@ int image_to_grid(const Geometry& g, const float2* W, float2* grid,
     return st;
 }
 
+// Whole-grid 2-D FFT in place, unnormalised (rocFFT / cuFFT convention:
+// forward e^-, inverse e^+): rows, then the four-step columns; the output
+// rows are stored permuted (k_cols_b_block).
+template<int N1, int N2>
+int fft2d_block(float2* grid, bool forward, const float2* W,
+        hipStream_t stream)
+{
+    constexpr int G = N1 * N2;
+    sdp_Error st = SDP_SUCCESS;
+    const size_t lds = row_lds_bytes(G);
+    if (forward)
+    {
+        SDP_HIP_CHECK((allow_lds<k_rows_image<G>>(lds)), &st);
+        if (st) return st;
+        k_rows_image<G><<<row_blocks(G), RowPlan<G>::P, lds, stream>>>(
+                grid, 0, G, W, nullptr, 0);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        if (st) return st;
+        k_cols_a_grid<N1, N2, -1><<<col_grid<k_cols_a_grid<N1, N2, -1>>(N1,
+                G, ColPlan<N2>::B), 256, kColLdsBytes, stream>>>(grid, G, W);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        if (st) return st;
+        k_cols_b_block<N1, N2, -1><<<col_grid<k_cols_b_block<N1, N2, -1>>(
+                N2, G, ColPlan<N1>::B), 256, kColLdsBytes, stream>>>(grid, G,
+                W);
+    }
+    else
+    {
+        SDP_HIP_CHECK((allow_lds<k_rows_grid<G>>(lds)), &st);
+        if (st) return st;
+        k_rows_grid<G><<<row_blocks(G), RowPlan<G>::P, lds, stream>>>(
+                grid, 0, G, W, nullptr, 0);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        if (st) return st;
+        k_cols_a_grid<N1, N2, 1><<<col_grid<k_cols_a_grid<N1, N2, 1>>(N1,
+                G, ColPlan<N2>::B), 256, kColLdsBytes, stream>>>(grid, G, W);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        if (st) return st;
+        k_cols_b_block<N1, N2, 1><<<col_grid<k_cols_b_block<N1, N2, 1>>(
+                N2, G, ColPlan<N1>::B), 256, kColLdsBytes, stream>>>(grid, G,
+                W);
+    }
+    SDP_HIP_CHECK_LAUNCH(&st);
+    return st;
+}
+
 // Dispatch on G = N1 * N2 (N2 = N1 or 2 * N1).
 #define SDP_ES_FFT_DISPATCH(G, CALL) \
     switch (G) \
@@ -1130,6 +1212,28 @@ int fft_image_to_grid(const ImageParams<float>& ip, const FftTwiddles& tw,
     const float2* W = (const float2*)tw.table;
     SDP_ES_FFT_DISPATCH(g.G, (image_to_grid<N1, N2>(g, W, (float2*)grid,
             tiles, ncoarse, stream)))
+}
+
+int fft2d_inplace_permuted(float* grid, int grid_size, bool forward,
+        const FftTwiddles& tw, hipStream_t stream)
+{
+    if (tw.G != grid_size) return SDP_ERR_INVALID_ARGUMENT;
+    const float2* W = (const float2*)tw.table;
+    SDP_ES_FFT_DISPATCH(grid_size, (fft2d_block<N1, N2>((float2*)grid,
+            forward, W, stream)))
+}
+
+int fft_perm_n2(int grid_size)
+{
+    switch (grid_size)
+    {
+    case 1024: return 32;
+    case 2048: return 64;
+    case 4096: return 64;
+    case 8192: return 128;
+    case 16384: return 128;
+    default: return 0;
+    }
 }
 
 } // namespace sdp_es

@@ -52,6 +52,7 @@
 #include "wtower_ops.h"
 #include "wtower_plan.h"
 #include "../fft/fft2d.h"
+#include "es_fft.h"
 #include "../utility/sdp_hip.h"
 
 using namespace sdp_wt;
@@ -573,7 +574,7 @@ template<typename T>
 __global__ void k_cut_out(const Cx<T>* __restrict__ grid, int64_t G,
         Cx<T>* __restrict__ wimg, int S, int64_t layer, const int* task,
         int64_t nv, int64_t min_iu, int64_t min_iv, int eff, int64_t slots,
-        int nbx)
+        int nbx, int perm_n2)
 {
     const int64_t slot = blockIdx.x / nbx;
     const int b = (int)(blockIdx.x % nbx) * (int)blockDim.x + (int)threadIdx.x;
@@ -601,7 +602,10 @@ __global__ void k_cut_out(const Cx<T>* __restrict__ grid, int64_t G,
     {
         int64_t gu = ou + a0 + r;
         if (gu >= G) gu -= G;
-        x[r] = (a0 + r < S) ? grid[gu * G + gv] : cx<T>(0, 0);
+        // Row gu of the FFT'd grid (stored permuted by the fused FFT).
+        x[r] = (a0 + r < S) ?
+                grid[sdp_es::fft_perm_row(gu, G, perm_n2) * G + gv] :
+                cx<T>(0, 0);
     }
 #pragma unroll
     for (int r = 0; r < kCutRows; ++r)
@@ -723,7 +727,7 @@ constexpr int kImgRows = 4;
 // checkerboard(IFFT(grid)) / G^2) (.cpp:702-711).
 template<typename T>
 __global__ void k_image_update(const Cx<T>* __restrict__ grid, int64_t G,
-        AnyView image, T norm, CorrParams cp)
+        AnyView image, T norm, CorrParams cp, int perm_n2)
 {
 #pragma clang fp contract(off)
     const int64_t gv = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -740,7 +744,8 @@ __global__ void k_image_update(const Cx<T>* __restrict__ grid, int64_t G,
         const int64_t gu = gu0 + r;
         const bool ok = gu < G;
         const int64_t i = (ok ? gu : 0) * G + gv;
-        x[r] = grid[i];
+        // Row gu of the FFT'd grid (stored permuted by the fused FFT).
+        x[r] = grid[sdp_es::fft_perm_row(ok ? gu : 0, G, perm_n2) * G + gv];
         o[r] = image.load(i);
         const int pl = (int)(gu - G / 2);
         sc[r] = (ok && corr_inside(pl, pm, cp)) ?
@@ -1696,6 +1701,32 @@ sdp_fft::Plan2D* cached_plan(int n, bool dbl, size_t batch, size_t dist,
     return p;
 }
 
+// The w-stack plane FFT (complex float, G a power of two in [1024, 16384]):
+// the fused three-pass FFT (es_fft.hip) in place, output rows permuted,
+// instead of rocFFT's four passes (env SDP_WT_FFT=rocfft keeps rocFFT).
+const sdp_es::FftTwiddles* plane_fft_twiddles(int64_t G, bool dbl,
+        sdp_Error* status)
+{
+    static int use = -1;
+    if (use < 0)
+    {
+        const char* e = getenv("SDP_WT_FFT");
+        use = (e && std::string(e) == "rocfft") ? 0 : 1;
+    }
+    if (!use || dbl || G > INT32_MAX || !sdp_es::fused_fft_supported((int)G))
+        return nullptr;
+    static std::map<int64_t, sdp_es::FftTwiddles> cache;
+    auto it = cache.find(G);
+    if (it != cache.end()) return &it->second;
+    sdp_es::FftTwiddles tw;
+    if (sdp_es::fft_twiddles_create((int)G, &tw) != 0)
+    {
+        *status = SDP_ERR_RUNTIME;
+        return nullptr;
+    }
+    return &(cache[G] = tw);
+}
+
 sdp_GridderWtowerUVW* cached_kernel(int image_size, int S, double theta,
         double w_step, double hu, double hv, int support, int os,
         int w_support, int wos, sdp_Error* status)
@@ -2373,12 +2404,26 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
         if (gr.last_of_plane)
         {
             const double ti = now_s();
-            sdp_fft::exec_2d(big, d_grid, false, 0, status);
+            const sdp_es::FftTwiddles* tw = plane_fft_twiddles(G,
+                    sizeof(T) == 8, status);
+            int perm_n2 = 0;
+            if (tw)
+            {
+                const int e = sdp_es::fft2d_inplace_permuted((float*)d_grid,
+                        (int)G, false, *tw, 0);
+                if (e) *status = (sdp_Error)e;
+                perm_n2 = sdp_es::fft_perm_n2((int)G);
+            }
+            else
+            {
+                sdp_fft::exec_2d(big, d_grid, false, 0, status);
+            }
             const CorrParams cp = corr_params_tab(k, (int)(gr.iw * g.H), true,
                     sizeof(T) == 4, status);
             k_image_update<T><<<dim3(blocks_of(G),
                     (unsigned)((G + kImgRows - 1) / kImgRows)), 256>>>(
-                    d_grid, G, image, (T)(1.0 / ((double)G * G)), cp);
+                    d_grid, G, image, (T)(1.0 / ((double)G * G)), cp,
+                    perm_n2);
             SDP_HIP_CHECK_LAUNCH(status);
             if (verbosity > 0)
             {
@@ -2470,6 +2515,10 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
     sdp_fft::Plan2D* big = cached_plan((int)G, sizeof(T) == 8, 1, G * G,
             status);
     if (*status) return;
+    const sdp_es::FftTwiddles* tw = plane_fft_twiddles(G, sizeof(T) == 8,
+            status);
+    if (*status) return;
+    const int perm_n2 = tw ? sdp_es::fft_perm_n2((int)G) : 0;
     const Cx<double>* wp = (const Cx<double>*)k->d_w_pattern;
     const int ws_n = g.w_support;
     const T norm = (T)(1.0 / ((double)g.S * g.S));
@@ -2485,7 +2534,16 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
                     (unsigned)((G + kImgRows - 1) / kImgRows)), 256>>>(
                     image, G, d_grid, cp);
             SDP_HIP_CHECK_LAUNCH(status);
-            sdp_fft::exec_2d(big, d_grid, true, 0, status);
+            if (tw)
+            {
+                const int e = sdp_es::fft2d_inplace_permuted((float*)d_grid,
+                        (int)G, true, *tw, 0);
+                if (e) *status = (sdp_Error)e;
+            }
+            else
+            {
+                sdp_fft::exec_2d(big, d_grid, true, 0, status);
+            }
             if (verbosity > 0)
             {
                 (void)hipDeviceSynchronize();
@@ -2512,7 +2570,8 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
             const int nbx = (g.S + 255) / 256;
             k_cut_out<T><<<dim3((unsigned)(gr.slots_alloc * nbx),
                     (unsigned)((g.S + kCutRows - 1) / kCutRows)), 256>>>(d_grid, G, d_wimg, g.S, layer,
-                    p.task, g.nv, g.min_iu, g.min_iv, g.eff, gr.slots, nbx);
+                    p.task, g.nv, g.min_iu, g.min_iv, g.eff, gr.slots, nbx,
+                    perm_n2);
         }
         sdp_fft::exec_2d(sp, d_wimg, false, 0, status);
         const int64_t first = gr.first_p + g.P0 - p.off_w;
