@@ -731,8 +731,17 @@ __global__ void k_image_update(const Cx<T>* __restrict__ grid, int64_t G,
 {
 #pragma clang fp contract(off)
     const int64_t gv = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t gu0 = (int64_t)blockIdx.y * kImgRows;
+    // blockIdx.y: kImgRows consecutive rows of the grid as stored; with the
+    // fused FFT's permuted rows (perm_n2 > 0), stored row s holds natural
+    // row (s % N1) N2 + s / N1, so the grid reads stay consecutive and the
+    // image rows of a thread are N2 apart.
+    const int64_t s0 = (int64_t)blockIdx.y * kImgRows;
     if (gv >= G) return;
+    auto natural = [&](int64_t s) -> int64_t {
+        if (!perm_n2) return s;
+        const int64_t n1 = G / perm_n2;
+        return (s % n1) * perm_n2 + s / n1;
+    };
     constexpr int kind = sizeof(T) == 8 ? 3 : 2;
     const int pm = (int)(gv - G / 2);
     Cx<T> x[kImgRows];
@@ -741,12 +750,11 @@ __global__ void k_image_update(const Cx<T>* __restrict__ grid, int64_t G,
 #pragma unroll
     for (int r = 0; r < kImgRows; ++r)
     {
-        const int64_t gu = gu0 + r;
-        const bool ok = gu < G;
-        const int64_t i = (ok ? gu : 0) * G + gv;
-        // Row gu of the FFT'd grid (stored permuted by the fused FFT).
-        x[r] = grid[sdp_es::fft_perm_row(ok ? gu : 0, G, perm_n2) * G + gv];
-        o[r] = image.load(i);
+        const int64_t st = s0 + r;
+        const bool ok = st < G;
+        const int64_t gu = natural(ok ? st : 0);
+        x[r] = grid[(ok ? st : 0) * G + gv];
+        o[r] = image.load(gu * G + gv);
         const int pl = (int)(gu - G / 2);
         sc[r] = (ok && corr_inside(pl, pm, cp)) ?
                 corr_scale(pl, pm, kind, cp) : 1.0;
@@ -754,8 +762,8 @@ __global__ void k_image_update(const Cx<T>* __restrict__ grid, int64_t G,
 #pragma unroll
     for (int r = 0; r < kImgRows; ++r)
     {
-        const int64_t gu = gu0 + r;
-        if (gu >= G) break;
+        if (s0 + r >= G) break;
+        const int64_t gu = natural(s0 + r);
         Cx<T> v = x[r];
         if (parity_sign(gu + gv) < 0)
         {
