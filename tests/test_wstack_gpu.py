@@ -189,7 +189,9 @@ def test_argument_errors(device, case):
 @pytest.mark.parametrize("degrid", [False, True])
 def test_fused_towers_match_double_precision(device, degrid):
     """Complex-float runs take the fused tower kernels (k_tower_dft /
-    k_tower_idft); checked against the complex-double (layer-by-layer) path
+    k_tower_idft) and, at this power-of-two image size, the fused in-place
+    plane FFT with permuted rows (es_fft.hip fft2d_inplace_permuted);
+    checked against the complex-double path (layer-by-layer towers, rocFFT)
     on a config-4-shaped case dense enough that the per-layer visibility
     windows of a sub-grid overflow the kernels' LDS ring (multi-piece
     windows, restaging, flushes of partial sums)."""
