@@ -1633,6 +1633,114 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
     }
 }
 
+// Degrid mode, ahead of k_gather_tab: each work item's records reordered
+// by the 16 x 16 sub-tile of their first tap (counting sort over the 16
+// keys, deterministic: key, then round, wave, lane), so that a chunk of
+// consecutive entries touches few of the 25 sub-tiles whose grid values the
+// gather loads (a chunk of unordered entries touches nearly all of them).
+// The piece is staged in LDS and written back in order, coalesced. Pieces
+// of more than kSortCap entries (hot tiles) are left as they are: the
+// small LDS footprint keeps 8 workgroups per CU on this memory-bound pass.
+constexpr int kSortCap = 1024;
+
+__global__ __launch_bounds__(256) void k_sort_pieces(EsParams<float> p,
+        float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
+        const uint32_t* __restrict__ item_start,
+        const uint32_t* __restrict__ item_bin)
+{
+    __shared__ float4 s_rec[kSortCap];
+    __shared__ uint16_t s_inv[kSortCap];     // slot -> entry
+    __shared__ uint32_t s_cnt[4][16];
+    __shared__ uint32_t s_run[16];
+    const uint32_t item = blockIdx.x;
+    if (item_bin[item] == kNoBin) return;
+    const int b = (int)item_bin[item];
+    const uint32_t piece = item - item_start[b];
+    const uint32_t e0 = bin_start[b] + piece * kPiece;
+    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
+    // One gather chunk: order is irrelevant; hot pieces: left unsorted.
+    if (e1 <= e0 + 256 || e1 > e0 + kSortCap) return;
+    const int n = (int)(e1 - e0);
+    const int half = p.G / 2;
+    int r0, c0;
+    tile_origin(p, b, r0, c0);
+    const int tu0 = r0 - half, tv0 = c0 - half;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    float4* r4 = (float4*)recs;
+    for (int i = t; i < n; i += 256) s_rec[i] = r4[e0 + i];
+    __syncthreads();
+    auto key_of = [&](int i) -> int {
+        if (i >= n) return -1;
+        const float4 r = s_rec[i];
+        int u0, u1, v0, v1;
+        tap_range(p, r.x, r.y, u0, u1, v0, v1);
+        const int kr = min(max((u0 - tu0) >> 4, 0), 3);
+        const int kc = min(max((v0 - tv0) >> 4, 0), 3);
+        return kr * 4 + kc;
+    };
+    // Pass 1: per-key totals (lane k of each wave accumulates key k).
+    constexpr int kRounds = kSortCap / 256;
+    int keys[kRounds];
+#pragma unroll
+    for (int rd = 0; rd < kRounds; ++rd) keys[rd] = key_of(rd * 256 + t);
+    const int rounds = (n + 255) / 256;
+    uint32_t tot = 0;
+#pragma unroll
+    for (int rd = 0; rd < kRounds; ++rd)
+    {
+        if (rd >= rounds) break;
+        const int key = keys[rd];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+        {
+            const uint64_t m = __ballot(key == k);
+            if (lane == k) tot += (uint32_t)__popcll(m);
+        }
+    }
+    if (lane < 16) s_cnt[wave][lane] = tot;
+    __syncthreads();
+    if (t == 0)
+    {
+        uint32_t run = 0;
+        for (int k = 0; k < 16; ++k)
+        {
+            s_run[k] = run;
+            run += s_cnt[0][k] + s_cnt[1][k] + s_cnt[2][k] + s_cnt[3][k];
+        }
+    }
+    __syncthreads();
+    // Pass 2: slots.
+#pragma unroll
+    for (int rd = 0; rd < kRounds; ++rd)
+    {
+        if (rd >= rounds) break;
+        const int i = rd * 256 + t;
+        const int key = keys[rd];
+        uint32_t c = 0, rk = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+        {
+            const uint64_t m = __ballot(key == k);
+            if (lane == k) c = (uint32_t)__popcll(m);
+            if (key == k) rk = (uint32_t)__popcll(m & lt);
+        }
+        if (lane < 16) s_cnt[wave][lane] = c;
+        __syncthreads();
+        if (key >= 0)
+        {
+            uint32_t pos = s_run[key] + rk;
+            for (int w = 0; w < wave; ++w) pos += s_cnt[w][key];
+            s_inv[pos] = (uint16_t)i;
+        }
+        __syncthreads();
+        if (t < 16)
+            s_run[t] += s_cnt[0][t] + s_cnt[1][t] + s_cnt[2][t] + s_cnt[3][t];
+        __syncthreads();
+    }
+    for (int j = t; j < n; j += 256) r4[e0 + j] = s_rec[s_inv[j]];
+}
+
 // Degrid mode: one workgroup per work item; the tile plus its support halo
 // is staged in LDS once. Records are loaded 64 per wave; taps of four
 // entries are evaluated cooperatively; each entry is gathered by the whole
@@ -2051,6 +2159,19 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     return *status;
 }
 
+// Degrid records sorted by first-tap sub-tile inside each work item before
+// k_gather_tab (env SDP_ES_SORT_PIECES=0 disables).
+bool sort_pieces()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("SDP_ES_SORT_PIECES");
+        v = e ? atoi(e) : 1;
+    }
+    return v != 0;
+}
+
 template<typename T>
 int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         const T* grid, T* vis, hipStream_t stream)
@@ -2060,6 +2181,12 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     if constexpr (sizeof(T) == 4)
     {
         const float* recs = (const float*)s.recs;
+        if (use_tap_tables() && p.support <= 8 && sort_pieces())
+        {
+            k_sort_pieces<<<n_items, 256, 0, stream>>>(p,
+                    (float*)s.recs, s.bin_start, s.item_start, s.item_bin);
+            SDP_HIP_CHECK_LAUNCH(status);
+        }
         if (!use_tap_tables())
             ;
         else if (p.support <= 8 && p.do_w)

@@ -56,6 +56,11 @@ CASES = [
     # several chunk slots, walked XCD by XCD (k_scan_columns)
     (False, False, 600000, 1, 256, 1e-5),
     (False, True, 150000, 4, 256, 1e-5),
+    # 256 < entries per tile <= 1024: degrid pieces sorted by first-tap
+    # sub-tile before the gather (k_sort_pieces)
+    (False, False, 20000, 1, 256, 1e-5),
+    (False, True, 8000, 2, 256, 1e-5),
+    (False, False, 100000, 1, 840, 0.05),
 ]
 
 
