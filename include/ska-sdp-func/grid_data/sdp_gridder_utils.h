@@ -161,6 +161,83 @@ void sdp_gridder_clamp_channels_uv(
         sdp_Error* status
 );
 
+/* Number of non-zero pixels (complex: either part) of a 2-D image of
+ * shape[0] rows, .h:54-57 (impl .cpp:106-123, 987-1013). Runs on the GPU
+ * (host images are staged). */
+int64_t sdp_gridder_count_nonzero_pixels(
+        const sdp_Mem* image,
+        sdp_Error* status
+);
+
+/* vis[i, c] += sum_s flux[s] exp(-2 pi i (l u + m v + n w)) with (u, v, w)
+ * the row's coordinates in wavelengths at channel c minus the sub-grid
+ * offsets / theta (w: offset * w_step); a row is skipped when start_chs
+ * and end_chs are given and start >= end. Types: double lmn / uvw, complex
+ * double vis, or the float triple; flux double. .h:99-114 (impl
+ * .cpp:126-212, 1042-1100). Runs on the GPU. */
+void sdp_gridder_dft(
+        const sdp_Mem* uvws,
+        const sdp_Mem* start_chs,
+        const sdp_Mem* end_chs,
+        const sdp_Mem* flux,
+        const sdp_Mem* lmn,
+        int subgrid_offset_u,
+        int subgrid_offset_v,
+        int subgrid_offset_w,
+        double theta,
+        double w_step,
+        double freq0_hz,
+        double dfreq_hz,
+        sdp_Mem* vis,
+        sdp_Error* status
+);
+
+/* image[il, im] += taper[il] taper[im] sum_(i, c) vis[i, c]
+ * exp(+2 pi i (l u + m v + n w)) with lmn[il * size + im] the pixel's
+ * direction cosines (complex image, same precision as vis / uvw / lmn).
+ * .h:140-156 (impl .cpp:215-314, 1103-1239). Runs on the GPU. */
+void sdp_gridder_idft(
+        const sdp_Mem* uvws,
+        const sdp_Mem* vis,
+        const sdp_Mem* start_chs,
+        const sdp_Mem* end_chs,
+        const sdp_Mem* lmn,
+        const sdp_Mem* image_taper_1d,
+        int subgrid_offset_u,
+        int subgrid_offset_v,
+        int subgrid_offset_w,
+        double theta,
+        double w_step,
+        double freq0_hz,
+        double dfreq_hz,
+        sdp_Mem* image,
+        sdp_Error* status
+);
+
+/* (l, m, n) of every pixel (flux NULL) or of the non-zero pixels with
+ * their (tapered) real values in flux; l = (il - size / 2) theta / size.
+ * Host (CPU) output tables, as in the reference. .h:181-190 (impl
+ * .cpp:317-382, 1242-1302). */
+void sdp_gridder_image_to_flmn(
+        const sdp_Mem* image,
+        double theta,
+        double shear_u,
+        double shear_v,
+        const sdp_Mem* image_taper_1d,
+        sdp_Mem* flux,
+        sdp_Mem* lmn,
+        sdp_Error* status
+);
+
+/* out = a - b (out in CPU memory, same type as a), .h:260-265 (impl
+ * .cpp:429-458, 1383-1466). */
+void sdp_gridder_residual(
+        const sdp_Mem* a,
+        const sdp_Mem* b,
+        sdp_Mem* out,
+        sdp_Error* status
+);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,7 +57,8 @@ static void visit_f32(
         int do_w, int mode, int G, int support, float beta, float uv_scale,
         float w_scale, float min_plane_w, int plane,
         const float* uvw_row, float freq, const float vis_w[2],
-        double* grid_acc, const double* grid_in, double out[2])
+        double* grid_acc, const double* grid_in, double out[2],
+        int row_lo, int row_hi)
 {
     const float flip = do_w ? ((uvw_row[2] < 0.0f) ? -1.0f : 1.0f) : 1.0f;
     const float inv_wavelength = flip * freq / (float)C_LIGHT;
@@ -94,6 +95,7 @@ static void visit_f32(
     const int off = G / 2;
     for (int u = u_min; u <= u_max; ++u)
     {
+        if (u < row_lo || u > row_hi) continue;
         for (int v = v_min; v <= v_max; ++v)
         {
             float k = ku[u - u_min] * kv[v - v_min] * kw;
@@ -119,7 +121,8 @@ static void visit_f64(
         int do_w, int mode, int G, int support, double beta, double uv_scale,
         double w_scale, double min_plane_w, int plane,
         const double* uvw_row, double freq, const double vis_w[2],
-        double* grid_acc, const double* grid_in, double out[2])
+        double* grid_acc, const double* grid_in, double out[2],
+        int row_lo, int row_hi)
 {
     const double flip = do_w ? ((uvw_row[2] < 0.0) ? -1.0 : 1.0) : 1.0;
     const double inv_wavelength = flip * freq / C_LIGHT;
@@ -156,6 +159,7 @@ static void visit_f64(
     const int off = G / 2;
     for (int u = u_min; u <= u_max; ++u)
     {
+        if (u < row_lo || u > row_hi) continue;
         for (int v = v_min; v <= v_max; ++v)
         {
             double k = ku[u - u_min] * kv[v - v_min] * kw;
@@ -198,7 +202,7 @@ void oracle_es_grid_f32(
             double dummy[2];
             visit_f32(do_w, 0, G, support, beta, uv_scale, w_scale,
                     min_plane_w, plane, uvw + 3 * r, freq[c], vw, grid, 0,
-                    dummy);
+                    dummy, INT32_MIN, INT32_MAX);
         }
     }
 }
@@ -218,7 +222,7 @@ void oracle_es_grid_f64(
             double dummy[2];
             visit_f64(do_w, 0, G, support, beta, uv_scale, w_scale,
                     min_plane_w, plane, uvw + 3 * r, freq[c], vw, grid, 0,
-                    dummy);
+                    dummy, INT32_MIN, INT32_MAX);
         }
     }
 }
@@ -243,7 +247,7 @@ void oracle_es_degrid_f32(
             double o[2];
             visit_f32(do_w, 1, G, support, beta, uv_scale, w_scale,
                     min_plane_w, plane, uvw + 3 * r, freq[c], zero, 0, grid,
-                    o);
+                    o, INT32_MIN, INT32_MAX);
             out_vis[2 * i] += o[0];
             out_vis[2 * i + 1] += o[1];
         }
@@ -266,12 +270,131 @@ void oracle_es_degrid_f64(
             double o[2];
             visit_f64(do_w, 1, G, support, beta, uv_scale, w_scale,
                     min_plane_w, plane, uvw + 3 * r, freq[c], zero, 0, grid,
-                    o);
+                    o, INT32_MIN, INT32_MAX);
             out_vis[2 * i] += o[0];
             out_vis[2 * i + 1] += o[1];
         }
     }
 }
+
+/*
+ * Same result as oracle_es_grid_f32 / _f64 (identical taps, double
+ * accumulation, each cell's contributions summed in visibility order), but
+ * multi-threaded for the full-size parity tests: grid rows are split into
+ * stripes, visibilities are binned by the stripes their u taps touch, and
+ * each stripe is accumulated by one thread restricted to its rows.
+ */
+#define U_SPAN(FT, CEIL, FLOOR)                                              \
+    const FT flip = do_w ? ((uvw[3 * r + 2] < (FT)0) ? (FT)-1 : (FT)1)      \
+                         : (FT)1;                                            \
+    const FT inv_wl = flip * freq[c] / (FT)C_LIGHT;                          \
+    const FT hs = (FT)support / (FT)2;                                       \
+    const FT pu = uvw[3 * r] * inv_wl * uv_scale;                            \
+    const FT pw = do_w ? (uvw[3 * r + 2] * inv_wl - min_plane_w) * w_scale   \
+                       : (FT)0;                                              \
+    int u0 = (int)CEIL(pu - hs), u1 = (int)FLOOR(pu + hs);                   \
+    int w0 = (int)CEIL(pw - hs), w1 = (int)FLOOR(pw + hs);                   \
+    if (u0 < -(G / 2)) u0 = -(G / 2);                                        \
+    if (u1 > (G - 1) / 2) u1 = (G - 1) / 2;                                  \
+    if (w0 < plane) w0 = plane;                                              \
+    if (w1 > plane) w1 = plane;                                              \
+    const int skip = (w0 > w1 || u0 > u1);
+
+#define GRID_PAR(NAME, FT, VISIT, CEIL, FLOOR)                               \
+int NAME(int64_t num_rows, int num_chan, const FT* uvw, const FT* freq,      \
+        const FT* vis, const FT* weight, int G, int support, FT beta,        \
+        FT uv_scale, FT w_scale, FT min_plane_w, int do_w, int plane,        \
+        double* grid)                                                        \
+{                                                                            \
+    int nth = 1;                                                             \
+    _OMP_MAXTHREADS(nth);                                                    \
+    const int64_t nvis = num_rows * num_chan;                                \
+    const int ns = 4 * nth;                                                  \
+    const int rows_per = (G + ns - 1) / ns;                                  \
+    const int off = G / 2;                                                   \
+    int64_t* cnt = (int64_t*)calloc((size_t)nth * ns, sizeof(int64_t));      \
+    int64_t* start = (int64_t*)calloc((size_t)ns + 1, sizeof(int64_t));      \
+    if (!cnt || !start) return -1;                                           \
+    _Pragma("omp parallel")                                                  \
+    {                                                                        \
+        int tid = 0;                                                         \
+        _OMP_TID(tid);                                                       \
+        int64_t* my = cnt + (size_t)tid * ns;                                \
+        _Pragma("omp for schedule(static)")                                  \
+        for (int64_t i = 0; i < nvis; ++i)                                   \
+        {                                                                    \
+            const int64_t r = i / num_chan;                                  \
+            const int c = (int)(i - r * num_chan);                           \
+            U_SPAN(FT, CEIL, FLOOR)                                          \
+            if (skip) continue;                                              \
+            for (int s = (u0 + off) / rows_per; s <= (u1 + off) / rows_per;  \
+                    ++s)                                                     \
+                my[s]++;                                                     \
+        }                                                                    \
+    }                                                                        \
+    int64_t total = 0;                                                       \
+    for (int s = 0; s < ns; ++s)                                             \
+    {                                                                        \
+        start[s] = total;                                                    \
+        for (int t = 0; t < nth; ++t)                                        \
+        {                                                                    \
+            const int64_t n = cnt[(size_t)t * ns + s];                       \
+            cnt[(size_t)t * ns + s] = total;                                 \
+            total += n;                                                      \
+        }                                                                    \
+    }                                                                        \
+    start[ns] = total;                                                       \
+    int64_t* list = (int64_t*)malloc((size_t)(total > 0 ? total : 1) *      \
+            sizeof(int64_t));                                                \
+    if (!list) return -1;                                                    \
+    _Pragma("omp parallel")                                                  \
+    {                                                                        \
+        int tid = 0;                                                         \
+        _OMP_TID(tid);                                                       \
+        int64_t* my = cnt + (size_t)tid * ns;                                \
+        _Pragma("omp for schedule(static)")                                  \
+        for (int64_t i = 0; i < nvis; ++i)                                   \
+        {                                                                    \
+            const int64_t r = i / num_chan;                                  \
+            const int c = (int)(i - r * num_chan);                           \
+            U_SPAN(FT, CEIL, FLOOR)                                          \
+            if (skip) continue;                                              \
+            for (int s = (u0 + off) / rows_per; s <= (u1 + off) / rows_per;  \
+                    ++s)                                                     \
+                list[my[s]++] = i;                                           \
+        }                                                                    \
+    }                                                                        \
+    _Pragma("omp parallel for schedule(dynamic, 1)")                         \
+    for (int s = 0; s < ns; ++s)                                             \
+    {                                                                        \
+        const int lo = s * rows_per - off, hi = lo + rows_per - 1;           \
+        for (int64_t e = start[s]; e < start[s + 1]; ++e)                    \
+        {                                                                    \
+            const int64_t i = list[e];                                       \
+            const int64_t r = i / num_chan;                                  \
+            const int c = (int)(i - r * num_chan);                           \
+            FT vw[2] = { vis[2 * i] * weight[i], vis[2 * i + 1] * weight[i] };\
+            double dummy[2];                                                 \
+            VISIT(do_w, 0, G, support, beta, uv_scale, w_scale, min_plane_w, \
+                    plane, uvw + 3 * r, freq[c], vw, grid, 0, dummy, lo, hi);\
+        }                                                                    \
+    }                                                                        \
+    free(list);                                                              \
+    free(start);                                                             \
+    free(cnt);                                                               \
+    return nth;                                                              \
+}
+
+#ifdef _OPENMP
+#define _OMP_MAXTHREADS(n) (n) = omp_get_max_threads()
+#define _OMP_TID(t) (t) = omp_get_thread_num()
+#else
+#define _OMP_MAXTHREADS(n) (void)(n)
+#define _OMP_TID(t) (void)(t)
+#endif
+
+GRID_PAR(oracle_es_grid_f32_par, float, visit_f32, ceilf, floorf)
+GRID_PAR(oracle_es_grid_f64_par, double, visit_f64, ceil, floor)
 
 /*
  * CPU baseline leg (bench.py only): a multi-threaded CPU gridder of the

@@ -74,6 +74,12 @@ def lib():
         _lib.oracle_es_grid_f32_omp.argtypes = [i64, i32, P, P, P, P, i32,
                                                 i32, f32, f32, P]
         _lib.oracle_es_grid_f32_omp.restype = i32
+        _lib.oracle_es_grid_f32_par.argtypes = \
+            _lib.oracle_es_grid_f32.argtypes
+        _lib.oracle_es_grid_f32_par.restype = i32
+        _lib.oracle_es_grid_f64_par.argtypes = \
+            _lib.oracle_es_grid_f64.argtypes
+        _lib.oracle_es_grid_f64_par.restype = i32
     return _lib
 
 
@@ -176,7 +182,10 @@ def scatter(geo, uvw, freq, vis, weight, plane=0):
     freq = np.ascontiguousarray(freq)
     vis = np.ascontiguousarray(vis)
     weight = np.ascontiguousarray(weight)
-    fn = lib().oracle_es_grid_f64 if dbl else lib().oracle_es_grid_f32
+    # Stripe-parallel form: the same taps and, per cell, the same summation
+    # order as the serial oracle_es_grid_f32/_f64 (es_oracle.c).
+    fn = (lib().oracle_es_grid_f64_par if dbl
+          else lib().oracle_es_grid_f32_par)
     fn(R, C, _ptr(uvw), _ptr(freq), _ptr(vis), _ptr(weight), G,
        geo["support"], beta, uvs, ws, mpw, int(geo["do_w"]), plane,
        _ptr(grid))
@@ -194,6 +203,28 @@ def gather(geo, uvw, freq, grid, out_vis, plane=0):
     fn(R, C, _ptr(np.ascontiguousarray(uvw)),
        _ptr(np.ascontiguousarray(freq)), _ptr(grid), G, geo["support"],
        beta, uvs, ws, mpw, int(geo["do_w"]), plane, _ptr(out_vis))
+
+
+def _workers():
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+
+
+def _ifft2(grid):
+    """Unnormalised inverse 2-D FFT in float64 (pocketfft, threaded)."""
+    try:
+        import scipy.fft
+        return scipy.fft.ifft2(grid, norm="forward", workers=_workers())
+    except ImportError:
+        return np.fft.ifft2(grid, norm="forward")
+
+
+def _fft2(grid):
+    """Unnormalised forward 2-D FFT in float64 (pocketfft, threaded)."""
+    try:
+        import scipy.fft
+        return scipy.fft.fft2(grid, workers=_workers())
+    except ImportError:
+        return np.fft.fft2(grid)
 
 
 def _rt(dirty_or_vis):
@@ -216,7 +247,7 @@ def grid_uvw_es_fft(geo, uvw, freq, vis, weight, dirty_in):
     sgn = _checker(n).astype(rt)
     for plane in range(geo["num_w_planes"]):
         grid = scatter(geo, uvw, freq, vis, weight, plane)
-        layer = np.fft.ifft2(grid, norm="forward")      # unnormalised, +i
+        layer = _ifft2(grid)                            # unnormalised, +i
         sub = layer[sl, sl]
         re = sub.real.astype(rt)
         im = sub.imag.astype(rt)
@@ -252,7 +283,7 @@ def ifft_degrid_uvw_es(geo, uvw, freq, dirty_in, num_chan=None):
                 pi * img).astype(np.float64)
         else:
             grid[sl, sl] = img
-        grid = np.fft.fft2(grid)                         # unnormalised, -i
+        grid = _fft2(grid)                               # unnormalised, -i
         gather(geo, uvw, freq, grid, out, plane)
     return out, dirty
 

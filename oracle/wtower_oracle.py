@@ -716,3 +716,121 @@ def wstack_degrid_all(image, f0, df, uvw, S, theta, w_step, shear_u,
                 plan.degrid(sub, iu * eff, iv * eff, off_w, f0, df, uvw, su,
                             eu, vis)
     return vis
+
+
+# -- stand-alone grid corrections (sdp_gridder_grid_correct.cpp) ----------
+
+def grid_correct_pswf(image_size, theta, w_step, shear_u, shear_v, support,
+                      w_support, facet, off_l, off_m):
+    """grid_corr_pswf<T> (sdp_gridder_grid_correct.cpp:18-73, public
+    :119-243): facet /= pswf(l) pswf(m) pswf_n(n), the scale formed in
+    double and applied in the facet's precision; returns a new array."""
+    N = image_size
+    pswf_lm = generate_pswf(support * (np.pi / 2), N, True)
+    c_n = w_support * (np.pi / 2)
+    nl, nm = facet.shape
+    pl = np.arange(nl) - nl // 2 + off_l
+    pm = np.arange(nm) - nm // 2 + off_m
+    l = pl * theta / N
+    m = pm * theta / N
+    n = lm_to_n(l[:, None], m[None, :], shear_u, shear_v)
+    n_x = np.abs(n * 2.0 * w_step)
+    pswf_n = np.ones_like(n_x)
+    if c_n > 0:
+        inside = n_x < 1.0
+        if np.any(inside):
+            pswf_n[inside] = pswf_values(c_n, n_x[inside])
+    scale = 1.0 / (pswf_lm[pl + N // 2][:, None]
+                   * pswf_lm[pm + N // 2][None, :] * pswf_n)
+    real = np.float32 if facet.dtype in (np.float32, np.complex64) \
+        else np.float64
+    return (facet * scale.astype(real)).astype(facet.dtype)
+
+
+def grid_correct_w_stack(image_size, theta, w_step, shear_u, shear_v, facet,
+                         off_l, off_m, w_offset, inverse):
+    """grid_corr_w_stack<T> (sdp_gridder_grid_correct.cpp:77-114): facet
+    *= exp(2 pi i w_step n w_offset), or its inverse when not inverse;
+    returns a new array."""
+    if w_offset == 0:
+        return facet.copy()
+    N = image_size
+    nl, nm = facet.shape
+    l = (np.arange(nl) - nl // 2 + off_l) * theta / N
+    m = (np.arange(nm) - nm // 2 + off_m) * theta / N
+    n = lm_to_n(l[:, None], m[None, :], shear_u, shear_v)
+    phase = 2.0 * np.pi * w_step * n * w_offset
+    w = np.cos(phase) + 1j * np.sin(phase)
+    w = w if inverse else 1.0 / w
+    return (facet * w.astype(facet.dtype)).astype(facet.dtype)
+
+
+# -- direct transforms of sdp_gridder_utils.cpp ----------------------------
+
+def dft_vis(uvws, start_chs, end_chs, flux, lmn, off_u, off_v, off_w, theta,
+            w_step, f0, df, vis):
+    """dft<> (sdp_gridder_utils.cpp:126-212): vis += sum_s flux_s
+    exp(-2 pi i (l u + m v + n w)); a row with start >= end is skipped."""
+    du = dv = dw = 0.0
+    if theta > 0:
+        du, dv, dw = off_u / theta, off_v / theta, off_w * w_step
+    out = vis.astype(np.complex128)
+    rows, nchan = vis.shape
+    live = np.ones(rows, bool) if start_chs is None else \
+        (np.asarray(start_chs) < np.asarray(end_chs))
+    uvw = np.asarray(uvws, np.float64)
+    for c in range(nchan):
+        inv = (f0 + df * c) / C_0
+        u = uvw[:, 0] * inv - du
+        v = uvw[:, 1] * inv - dv
+        w = uvw[:, 2] * inv - dw
+        ph = -2.0 * np.pi * (np.outer(u, lmn[:, 0]) + np.outer(v, lmn[:, 1])
+                             + np.outer(w, lmn[:, 2]))
+        out[live, c] += (np.exp(1j * ph) @ np.asarray(flux, np.float64))[live]
+    return out
+
+
+def idft_image(uvws, vis, start_chs, end_chs, lmn, taper, off_u, off_v,
+               off_w, theta, w_step, f0, df, image):
+    """idft<> (sdp_gridder_utils.cpp:215-314): image[s] += taper
+    sum_(i, c) vis exp(+2 pi i (l u + m v + n w)) at lmn[s]."""
+    du = dv = dw = 0.0
+    if theta > 0:
+        du, dv, dw = off_u / theta, off_v / theta, off_w * w_step
+    size = image.shape[0]
+    live = np.ones(len(uvws), bool) if start_chs is None else \
+        (np.asarray(start_chs) < np.asarray(end_chs))
+    uvw = np.asarray(uvws, np.float64)[live]
+    vv = np.asarray(vis, np.complex128)[live]
+    acc = np.zeros(size * size, np.complex128)
+    for c in range(vv.shape[1]):
+        inv = (f0 + df * c) / C_0
+        u = uvw[:, 0] * inv - du
+        v = uvw[:, 1] * inv - dv
+        w = uvw[:, 2] * inv - dw
+        ph = 2.0 * np.pi * (np.outer(lmn[:size * size, 0], u)
+                            + np.outer(lmn[:size * size, 1], v)
+                            + np.outer(lmn[:size * size, 2], w))
+        acc += np.exp(1j * ph) @ vv[:, c]
+    t = np.ones(size) if taper is None else np.asarray(taper)
+    out = image.astype(np.complex128) + acc.reshape(size, size) * np.outer(
+        t, t)
+    return out
+
+
+def image_to_flmn(image, theta, shear_u, shear_v, taper=None,
+                  with_flux=True):
+    """image_to_flmn<> (sdp_gridder_utils.cpp:317-382): (flux, lmn) of the
+    non-zero pixels in row-major order, or lmn of every pixel."""
+    nl, nm = image.shape
+    l = (np.arange(nl) - nl // 2) * theta / nl
+    m = (np.arange(nm) - nm // 2) * theta / nm
+    L, M = np.meshgrid(l, m, indexing="ij")
+    N = lm_to_n(L, M, shear_u, shear_v)
+    t = np.ones(max(nl, nm)) if taper is None else np.asarray(taper)
+    T = np.outer(t[:nl], t[:nm])
+    if with_flux:
+        sel = image != 0
+        return ((image.real * T)[sel],
+                np.stack([L[sel], M[sel], N[sel]], axis=1))
+    return None, np.stack([L.ravel(), M.ravel(), N.ravel()], axis=1)

@@ -468,7 +468,9 @@ __global__ __launch_bounds__(NT) void k_bucket_fill(EsParams<T> p,
     // lanes = consecutive channels of a row), so the vis / weight loads of
     // a wave are coalesced for any channel count; the row's uvw is an L1
     // hit shared by its channels.
-    const uint32_t nvis = (uint32_t)((r1 - r0) * num_chan);
+    // Trailing chunks can be empty (r0 >= num_rows when the rows do not
+    // fill all num_chunks chunks of ceil(rows / chunks) rows).
+    const uint32_t nvis = r1 > r0 ? (uint32_t)((r1 - r0) * num_chan) : 0u;
     for (uint32_t li = threadIdx.x; li < nvis; li += NT)
     {
         const uint32_t rl = num_chan == 1 ? li : li / (uint32_t)num_chan;

@@ -47,6 +47,95 @@ int sturm_count(const std::vector<double>& d, const std::vector<double>& e,
 
 } // namespace
 
+namespace {
+
+// Lowest eigenpair of the symmetric tridiagonal (d, e): Sturm bisection for
+// the eigenvalue, then inverse iteration; returns the unit eigenvector.
+std::vector<double> lowest_eigenvector(const std::vector<double>& d,
+        const std::vector<double>& e)
+{
+    const int n = (int)d.size();
+    double lo = 1e300, hi = -1e300;
+    for (int k = 0; k < n; ++k)
+    {
+        const double rad = std::fabs(k > 0 ? e[k - 1] : 0.0) + std::fabs(e[k]);
+        lo = std::min(lo, d[k] - rad);
+        hi = std::max(hi, d[k] + rad);
+    }
+    for (int it = 0; it < 200; ++it)
+    {
+        const double mid = 0.5 * (lo + hi);
+        if (mid == lo || mid == hi) break;
+        if (sturm_count(d, e, mid) >= 1) hi = mid; else lo = mid;
+    }
+    const double lambda = 0.5 * (lo + hi);
+    std::vector<double> y(n, 1.0), b(n), cp(n), dp(n);
+    const double shift = lambda - 1e-10 * std::max(1.0, std::fabs(lambda));
+    for (int it = 0; it < 6; ++it)
+    {
+        b = y;
+        double den = d[0] - shift;
+        cp[0] = e[0] / den;
+        dp[0] = b[0] / den;
+        for (int k = 1; k < n; ++k)
+        {
+            den = (d[k] - shift) - e[k - 1] * cp[k - 1];
+            cp[k] = (k < n - 1) ? e[k] / den : 0.0;
+            dp[k] = (b[k] - e[k - 1] * dp[k - 1]) / den;
+        }
+        y[n - 1] = dp[n - 1];
+        for (int k = n - 2; k >= 0; --k) y[k] = dp[k] - cp[k] * y[k + 1];
+        double norm = 0.0;
+        for (int k = 0; k < n; ++k) norm += y[k] * y[k];
+        norm = std::sqrt(norm);
+        for (int k = 0; k < n; ++k) y[k] /= norm;
+    }
+    return y;
+}
+
+} // namespace
+
+Pswf make_pswf_order(double c, int m)
+{
+    if (m <= 0) return make_pswf(c);
+    // Prolate operator -d/dx (1 - x^2) d/dx + m^2 / (1 - x^2) + c^2 x^2 in
+    // the orthonormal basis of P_l^m, l = m, m + 2, ...: diagonal
+    // l (l + 1) + c^2 <x^2>_ll, off-diagonal c^2 a_l a_{l+1}, with
+    // x P_l^m = a_l P_{l+1}^m + a_{l-1} P_{l-1}^m (normalised),
+    // a_j = sqrt(((j + 1)^2 - m^2) / ((2j + 1)(2j + 3))).
+    const int n = std::max(40, (int)(c) + 40);
+    auto a = [m](double j) {
+        return std::sqrt(std::max(0.0, ((j + 1) * (j + 1) - (double)m * m) /
+                ((2 * j + 1) * (2 * j + 3))));
+    };
+    std::vector<double> d(n), e(n);
+    const double c2 = c * c;
+    for (int k = 0; k < n; ++k)
+    {
+        const double l = m + 2.0 * k;
+        const double am = (l - 1 >= m) ? a(l - 1) : 0.0;
+        d[k] = l * (l + 1) + c2 * (a(l) * a(l) + am * am);
+        e[k] = c2 * a(l) * a(l + 1);
+    }
+    const std::vector<double> y = lowest_eigenvector(d, e);
+    Pswf p;
+    p.c = c;
+    p.m = m;
+    p.coef.resize(n);
+    for (int k = 0; k < n; ++k)
+    {
+        const double l = m + 2.0 * k;
+        // normalised -> plain P_l^m: sqrt((2l + 1) / 2 (l - m)! / (l + m)!)
+        p.coef[k] = y[k] * std::sqrt((2 * l + 1) / 2.0 *
+                std::exp(std::lgamma(l - m + 1) - std::lgamma(l + m + 1)));
+    }
+    double target = 1.0;
+    for (int j = 1; j <= m; ++j) target *= (2.0 * j - 1.0);
+    const double at0 = p(0.0);
+    for (int k = 0; k < n; ++k) p.coef[k] *= target / at0;
+    return p;
+}
+
 Pswf make_pswf(double c)
 {
     Pswf p;
@@ -103,6 +192,26 @@ Pswf make_pswf(double c)
 
 double Pswf::operator()(double x) const
 {
+    if (m > 0)
+    {
+        // Sum of coef[k] P_{m+2k}^m(x): P_m^m = (2m - 1)!! (1 - x^2)^(m/2),
+        // P_{m+1}^m = (2m + 1) x P_m^m,
+        // (l - m + 1) P_{l+1}^m = (2l + 1) x P_l^m - (l + m) P_{l-1}^m.
+        double pmm = std::pow(std::max(0.0, 1.0 - x * x), 0.5 * m);
+        for (int j = 1; j <= m; ++j) pmm *= (2.0 * j - 1.0);
+        double p_prev = pmm, p_cur = (2.0 * m + 1) * x * pmm;
+        double sum = coef.empty() ? 0.0 : coef[0] * pmm;
+        const int lmax = m + 2 * ((int)coef.size() - 1);
+        for (int l = m + 1; l < lmax; ++l)
+        {
+            const double p_next = ((2.0 * l + 1) * x * p_cur -
+                    (l + m) * p_prev) / (l - m + 1);
+            p_prev = p_cur;
+            p_cur = p_next;
+            if ((l + 1 - m) % 2 == 0) sum += coef[(l + 1 - m) / 2] * p_cur;
+        }
+        return sum;
+    }
     // Sum of coef[k] P_2k(x), Legendre recurrence up to degree 2 (n - 1).
     double p_prev = 1.0, p_cur = x, sum = coef.empty() ? 0.0 : coef[0];
     const int nmax = 2 * ((int)coef.size() - 1);

@@ -21,11 +21,20 @@ namespace sdp_wt {
 struct Pswf
 {
     double c = 0.0;
-    std::vector<double> coef;   // coefficients of P_0, P_2, P_4, ...
+    int m = 0;                  // order (n = m)
+    // m = 0: coefficients of P_0, P_2, P_4, ...; m > 0: of the associated
+    // Legendre functions P_m^m, P_{m+2}^m, ... (no Condon-Shortley phase).
+    std::vector<double> coef;
     double operator()(double x) const;
 };
 
 Pswf make_pswf(double c);
+
+// S_mm(c, x) of order m >= 0 in Flammer's normalisation
+// (S_mm(c, 0) = P_m^m(0) = (2m - 1)!!), the function the reference's
+// sdp_pswf_create(m, c) evaluates (sdp_pswf.cpp:612-635). m = 0 is
+// make_pswf(c).
+Pswf make_pswf_order(double c, int m);
 
 // sdp_pswf.cpp:570-601: values on `size` points x = 2 i / size about the
 // centre; out[0] = 0 (1e-15 with end_correction and even size).

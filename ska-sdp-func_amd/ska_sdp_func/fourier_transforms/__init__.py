@@ -1,0 +1,9 @@
+"""FFT functions (reference: src/ska_sdp_func/fourier_transforms/
+__init__.py); the SwiFTly transforms are out of scope."""
+
+from .fft import Fft, padded_fft_size
+
+__all__ = ["Fft", "padded_fft_size"]
+from .pswf import Pswf, generate_pswf  # noqa: E402
+
+__all__ += ["Pswf", "generate_pswf"]

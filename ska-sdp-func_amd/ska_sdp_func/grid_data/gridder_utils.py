@@ -228,6 +228,81 @@ _I = ctypes.c_int
 _D = ctypes.c_double
 _I64 = ctypes.c_int64
 
+
+def _opt(x):
+    return Mem(x) if x is not None else None
+
+
+def count_nonzero_pixels(image) -> int:
+    """Number of non-zero pixels (sdp_gridder_count_nonzero_pixels,
+    reference sdp_gridder_utils.h:54)."""
+    return int(Lib.sdp_gridder_count_nonzero_pixels(Mem(image)))
+
+
+def dft(uvws, start_chs, end_chs, flux, lmn, subgrid_offset_u: int,
+        subgrid_offset_v: int, subgrid_offset_w: int, theta: float,
+        w_step: float, freq0_hz: float, dfreq_hz: float, vis):
+    """vis += direct Fourier sum of point sources (sdp_gridder_dft,
+    reference sdp_gridder_utils.h:99). start_chs / end_chs may be None."""
+    Lib.sdp_gridder_dft(Mem(uvws), _opt(start_chs), _opt(end_chs),
+                        Mem(flux), Mem(lmn), subgrid_offset_u,
+                        subgrid_offset_v, subgrid_offset_w, theta, w_step,
+                        freq0_hz, dfreq_hz, Mem(vis))
+
+
+def idft(uvws, vis, start_chs, end_chs, lmn, image_taper_1d,
+         subgrid_offset_u: int, subgrid_offset_v: int, subgrid_offset_w: int,
+         theta: float, w_step: float, freq0_hz: float, dfreq_hz: float,
+         image):
+    """image += direct inverse Fourier sum of the visibilities at the
+    pixel directions lmn (sdp_gridder_idft, reference
+    sdp_gridder_utils.h:140)."""
+    Lib.sdp_gridder_idft(Mem(uvws), Mem(vis), _opt(start_chs), _opt(end_chs),
+                         Mem(lmn), _opt(image_taper_1d), subgrid_offset_u,
+                         subgrid_offset_v, subgrid_offset_w, theta, w_step,
+                         freq0_hz, dfreq_hz, Mem(image))
+
+
+def image_to_flmn(image, theta: float, shear_u: float, shear_v: float,
+                  image_taper_1d, flux, lmn):
+    """Pixel direction cosines (and non-zero pixel fluxes when flux is
+    given) into host arrays (sdp_gridder_image_to_flmn, reference
+    sdp_gridder_utils.h:181)."""
+    Lib.sdp_gridder_image_to_flmn(Mem(image), theta, shear_u, shear_v,
+                                  _opt(image_taper_1d), _opt(flux), Mem(lmn))
+
+
+def residual(array_a, array_b, out):
+    """out = a - b, out a host array (sdp_gridder_residual, reference
+    sdp_gridder_utils.h:260)."""
+    Lib.sdp_gridder_residual(Mem(array_a), Mem(array_b), Mem(out))
+
+
+def grid_correct_pswf(image_size: int, theta: float, w_step: float,
+                      shear_u: float, shear_v: float, support: int,
+                      w_support: int, facet, facet_offset_l: int,
+                      facet_offset_m: int):
+    """facet /= pswf(l) pswf(m) pswf_n(n) (sdp_gridder_grid_correct_pswf,
+    reference sdp_gridder_grid_correct.h:31)."""
+    Lib.sdp_gridder_grid_correct_pswf(image_size, theta, w_step, shear_u,
+                                      shear_v, support, w_support,
+                                      Mem(facet), facet_offset_l,
+                                      facet_offset_m)
+
+
+def grid_correct_w_stack(image_size: int, theta: float, w_step: float,
+                         shear_u: float, shear_v: float, facet,
+                         facet_offset_l: int, facet_offset_m: int,
+                         w_offset: int, inverse: bool):
+    """facet *= exp(-+2 pi i w_step n w_offset)
+    (sdp_gridder_grid_correct_w_stack, reference
+    sdp_gridder_grid_correct.h:60)."""
+    Lib.sdp_gridder_grid_correct_w_stack(image_size, theta, w_step, shear_u,
+                                         shear_v, Mem(facet),
+                                         facet_offset_l, facet_offset_m,
+                                         w_offset, int(bool(inverse)))
+
+
 Lib.wrap_func(
     "sdp_gridder_clamp_channels_single",
     restype=None,
@@ -292,5 +367,47 @@ Lib.wrap_func(
     restype=None,
     argtypes=[_M, _D, _D, _M, _M, ctypes.POINTER(ctypes.c_double),
               ctypes.POINTER(ctypes.c_double)],
+    check_errcode=True,
+)
+Lib.wrap_func(
+    "sdp_gridder_count_nonzero_pixels",
+    restype=ctypes.c_int64,
+    argtypes=[_M],
+    check_errcode=True,
+)
+Lib.wrap_func(
+    "sdp_gridder_dft",
+    restype=None,
+    argtypes=[_M, _M, _M, _M, _M, _I, _I, _I, _D, _D, _D, _D, _M],
+    check_errcode=True,
+)
+Lib.wrap_func(
+    "sdp_gridder_idft",
+    restype=None,
+    argtypes=[_M, _M, _M, _M, _M, _M, _I, _I, _I, _D, _D, _D, _D, _M],
+    check_errcode=True,
+)
+Lib.wrap_func(
+    "sdp_gridder_image_to_flmn",
+    restype=None,
+    argtypes=[_M, _D, _D, _D, _M, _M, _M],
+    check_errcode=True,
+)
+Lib.wrap_func(
+    "sdp_gridder_residual",
+    restype=None,
+    argtypes=[_M, _M, _M],
+    check_errcode=True,
+)
+Lib.wrap_func(
+    "sdp_gridder_grid_correct_pswf",
+    restype=None,
+    argtypes=[_I, _D, _D, _D, _D, _I, _I, _M, _I, _I],
+    check_errcode=True,
+)
+Lib.wrap_func(
+    "sdp_gridder_grid_correct_w_stack",
+    restype=None,
+    argtypes=[_I, _D, _D, _D, _D, _M, _I, _I, _I, _I],
     check_errcode=True,
 )

@@ -61,6 +61,12 @@ CASES = [
     (False, False, 20000, 1, 256, 1e-5),
     (False, True, 8000, 2, 256, 1e-5),
     (False, False, 100000, 1, 840, 0.05),
+    # 140000 rows x 64 channels: the chunk count is capped (kMaxChunks
+    # 1024), chunks of ceil(140000 / 1024) = 137 rows, and the last three
+    # chunks start past the last row (empty; k_bucket_fill once read past
+    # the arrays for them)
+    (False, False, 140000, 64, 256, 1e-5),
+    (False, True, 140000, 64, 256, 1e-5),
 ]
 
 
