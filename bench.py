@@ -8,7 +8,8 @@ Workload (BASELINE.json configs[1]):
   Inputs are generated directly in HBM (seed 20251015 + 2 + rank).
 
 A step = one full sdp_grid_uvw_es_fft call through the C ABI (bucketing,
-LDS tile scatter, rocFFT inverse 8192^2, fused screen + grid correction).
+MFMA tile scatter, pruned fused inverse FFT 8192^2 with the screen and grid
+correction in its last pass).
 value = visibilities gridded per second over the whole job (all ranks).
 The degridding half of the config-2 round trip is timed afterwards with the
 same step count and reported in "degrid"; "roundtrip_mvis_s" = R / (t_grid +
@@ -17,11 +18,16 @@ t_degrid).
 Multi-GPU (torchrun, one process per GPU, RCCL): weak scaling -- every rank
 grids its own 10M rows (a row shard of the job) into a partial image, then
 the partial images are summed onto rank 0 with one RCCL reduce (default,
---reduce image: 5440^2 f32 = 118 MB) or the per-GPU grids are reduced before
-a single FFT on rank 0 (--reduce grid: 8192^2 c64 = 512 MiB). The collective
-is inside the timed region; with the image reduce, step k's reduce runs on
-RCCL's stream while step k + 1 grids into a second image buffer (every
-reduce completes before the clock stops; --no-overlap serialises them).
+--reduce image: 5440^2 f32 = 118 MB); step k's reduce runs on RCCL's stream
+while step k + 1 grids into a second image buffer (every reduce completes
+before the clock stops; --no-overlap serialises them). The north star's
+other form -- the per-GPU 8192^2 grids (512 MiB) reduced before a single
+FFT on rank 0 -- is timed after it and reported in "grid_reduce_mode".
+
+"config3": BASELINE config 3 at every N -- 10M rows x 64 channels IN TOTAL
+(1.0-1.49 GHz), rows sharded over the ranks, per-rank scatter into a
+private grid, one RCCL reduce of the grids, one FFT + screen + correction on
+rank 0 (strong scaling); the reduce is also timed alone ("reduce_ms").
 
 Roofline: the dominant hand-written kernel's algorithmic bytes per launch
 divided by its HIP-event duration (library timing on the launch stream).
@@ -55,6 +61,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=10_000_000)
     ap.add_argument("--no-degrid", action="store_true")
+    ap.add_argument("--no-config3", action="store_true",
+                    help="skip the config-3 measurement (10M rows x 64 "
+                         "channels in total, sharded, RCCL grid reduce)")
+    ap.add_argument("--c3-rows", type=int, default=10_000_000)
+    ap.add_argument("--c3-chan", type=int, default=64)
+    ap.add_argument("--c3-steps", type=int, default=3)
     ap.add_argument("--no-overlap", action="store_true",
                     help="multi-GPU: wait for each step's reduce before the "
                          "next step (default: reduce of step k overlaps "
@@ -101,6 +113,34 @@ def gridding_bytes(rows, chan, G, n):
             + n * n * (8 + 4) + 2 * n * n * 4)
 
 
+def host_cpus():
+    """CPUs this process may use, and the machine's count.
+
+    nproc / os.cpu_count() report every CPU of the host; a GPU box grants
+    each job a share of them (its affinity mask and cgroup CPU quota), and
+    running more threads than the share only time-slices them. The CPU
+    baselines use the share and report all three figures.
+    """
+    total = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = total
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        quota = None
+    usable = min(affinity, quota) if quota else affinity
+    env = os.environ.get("OMP_NUM_THREADS")
+    return {"nproc": total, "affinity": affinity, "cgroup_quota": quota,
+            "omp_num_threads_env": int(env) if env and env.isdigit() else None,
+            "usable": usable}
+
+
 def cpu_baseline(args, G, support, beta, uv_scale):
     """Oracle ('port') CPU gridder timed on the host cores.
 
@@ -116,8 +156,10 @@ def cpu_baseline(args, G, support, beta, uv_scale):
 
     from oracle import es_oracle
 
+    host = host_cpus()
+    threads = host["usable"]
     lib = es_oracle.lib()
-    threads = min(16, os.cpu_count() or 1)
+    lib.oracle_set_threads(threads)
     n_s = min(args.cpu_sample_rows, args.rows)
     rng = np.random.default_rng(20251015 + 2)
     px = 2.0 * np.pi / 180.0 / args.image
@@ -156,6 +198,7 @@ def cpu_baseline(args, G, support, beta, uv_scale):
         "value": args.rows * args.chan / t_job / 1e6,
         "unit": "Mvis/s",
         "cores": int(used),
+        "host_cpus": host,
         "kind": "port",
         "sample": (f"oracle/es_oracle.c stripe-binned OpenMP f32 scatter of "
                    f"{n_s} config-2 rows ({t_scatter:.3f} s"
@@ -163,8 +206,88 @@ def cpu_baseline(args, G, support, beta, uv_scale):
                       else "")
                    + f") + scipy pocketfft ifft2 {G}^2 c64 on {threads} "
                    f"threads + crop/checkerboard/correction "
-                   f"({t_fft_img:.3f} s)"),
+                   f"({t_fft_img:.3f} s); {int(used)} threads = the CPUs "
+                   f"this job may use (affinity {host['affinity']}, cgroup "
+                   f"quota {host['cgroup_quota']}) of the host's "
+                   f"{host['nproc']}"),
     }
+
+
+def run_config3(args, torch, dev, dist, world, rank):
+    """BASELINE config 3: 10M rows x 64 channels IN TOTAL, rows sharded
+    over the ranks, each rank scattering its shard into a private uv grid,
+    one RCCL reduce of the 8192^2 complex64 grids (512 MiB) onto rank 0,
+    then one FFT + screen + correction there (north star: reduce before the
+    FFT). With one GPU the whole call runs on it (no collective). A step
+    is one such sharded gridding of all 6.4e8 visibilities; the reduce is
+    also timed alone."""
+    from ska_sdp_func.grid_data import GridderUvwEsFft
+    from ska_sdp_func.grid_data.distributed import grid_sharded, shard_rows
+
+    r0, r1 = shard_rows(args.c3_rows, rank, world)
+    uvw, freq, vis, weight, px = make_inputs(
+        torch, dev, r1 - r0, args.c3_chan, args.image,
+        20251015 + 3 + rank)
+    dirty = torch.zeros((args.image, args.image), dtype=torch.float32,
+                        device=dev)
+    plan = GridderUvwEsFft(uvw, freq, vis, weight, dirty, px, px, args.eps,
+                           False)
+    plan.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    G = plan.grid_size
+    grid_buf = (torch.empty((G, G), dtype=torch.complex64, device=dev)
+                if world > 1 else None)
+
+    def step():
+        dirty.zero_()
+        if world == 1:
+            plan.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
+        else:
+            grid_sharded(plan, uvw, freq, vis, weight, dirty, dist,
+                         mode="grid", dst=0, grid_buf=grid_buf)
+
+    def sync():
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    step()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.c3_steps):
+        step()
+    sync()
+    t = time.perf_counter() - t0
+    reduce_ms = None
+    if dist is not None:
+        tt = torch.tensor([t], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt.item())
+        n_red = 3
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(n_red):
+            dist.reduce(grid_buf, dst=0)
+        sync()
+        reduce_ms = 1e3 * (time.perf_counter() - t0) / n_red
+    total = args.c3_rows * args.c3_chan
+    out = {
+        "workload": (f"ES-FFT gridding, {args.c3_rows} rows x "
+                     f"{args.c3_chan} chan in total (1.0-1.49 GHz), image "
+                     f"{args.image}^2, eps {args.eps}, grid {G}^2, support "
+                     f"{plan.support}, rows sharded over {world} GPU(s)"),
+        "mvis_s": round(total * args.c3_steps / t / 1e6, 3),
+        "ms_per_step": round(1e3 * t / args.c3_steps, 3),
+        "steps": args.c3_steps,
+        "scaling": "strong",
+        "reduce": ("RCCL reduce of the per-GPU 8192^2 complex64 grids "
+                   "(512 MiB) before one FFT on rank 0" if world > 1 else
+                   "none (one GPU)"),
+        "reduce_ms": round(reduce_ms, 3) if reduce_ms is not None else None,
+    }
+    del uvw, vis, weight, plan, grid_buf
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -252,6 +375,32 @@ def main():
     total_vis = args.rows * args.chan * world
     value = total_vis * args.steps / t_grid / 1e6
 
+    # Multi-GPU, the other reduce mode: the per-GPU grids summed before one
+    # FFT (north star form; 512 MiB per step), timed after the default.
+    grid_reduce = None
+    if world > 1 and args.reduce == "image" and not args.no_overlap:
+        gbuf = torch.empty((G, G), dtype=torch.complex64, device=dev)
+
+        def grid_step_gr():
+            dirty.zero_()
+            grid_sharded(plan, uvw, freq, vis, weight, dirty, dist,
+                         mode="grid", dst=0, grid_buf=gbuf)
+
+        grid_step_gr()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            grid_step_gr()
+        barrier()
+        t_gr = time.perf_counter() - t0
+        t = torch.tensor([t_gr], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_gr = float(t.item())
+        grid_reduce = {"mvis_s": round(total_vis * args.steps / t_gr / 1e6,
+                                       3),
+                       "ms_per_step": round(1e3 * t_gr / args.steps, 4)}
+        del gbuf
+
     # Per-phase device times (HIP events on the plan stream), in separate
     # calls so that the event synchronisation stays out of the timed loop.
     phase_steps = max(1, min(args.steps, 5))
@@ -334,6 +483,10 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    config3 = None
+    if not args.no_config3:
+        config3 = run_config3(args, torch, dev, dist, world, rank)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -391,6 +544,8 @@ def main():
                               / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             },
             "degrid": degrid,
+            "grid_reduce_mode": grid_reduce,
+            "config3": config3,
             "roundtrip_mvis_s": (round(total_vis / ((ms_per_step
                                                      + degrid["ms_per_step"])
                                                     * 1e-3) / 1e6, 3)

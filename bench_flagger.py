@@ -69,20 +69,23 @@ def cpu_baseline(vis_dev, args, kw):
     import numpy as np
     from oracle import flagger_oracle as fo
 
-    nb = min(args.cpu_sample_baselines, args.B)
+    from bench import host_cpus
+
+    host = host_cpus()
+    # at least 8 baselines per thread, so that every thread has work
+    nb = min(args.B, max(args.cpu_sample_baselines, 8 * host["usable"]))
     sample = np.ascontiguousarray(vis_dev[:, :nb].cpu().numpy())
     flags = np.zeros(sample.shape, np.int32)
-    threads = min(16, os.cpu_count() or 1)
-    os.environ["OMP_NUM_THREADS"] = str(threads)
-    fo.lib()
+    threads = fo.lib().oracle_flagger_set_threads(host["usable"])
     t0 = time.perf_counter()
     fo.flagger_dynamic_threshold(sample, flags, **kw)
     dt = time.perf_counter() - t0
     return {"value": round(sample.size / dt / 1e6, 3), "unit": "Mvis/s",
-            "cores": threads, "kind": "port",
+            "cores": threads, "host_cpus": host, "kind": "port",
             "sample": (f"oracle/flagger_oracle.c (OpenMP over baselines) on "
                        f"{nb} of {args.B} baselines x {args.T} x {args.C} x "
-                       f"{args.P} ({dt:.2f} s)")}
+                       f"{args.P} ({dt:.2f} s), {threads} threads = the CPUs "
+                       f"this job may use of the host's {host['nproc']}")}
 
 
 def main():

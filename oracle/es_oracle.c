@@ -32,6 +32,19 @@
 
 #define C_LIGHT 299792458.0
 
+/* Threads of the OpenMP loops below (the bench's CPU baseline sets the
+ * job's CPU share; returns the count in effect). */
+int oracle_set_threads(int n)
+{
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
+}
+
 /* ---- f32 path ---------------------------------------------------------- */
 
 static inline float es_f(float beta, float x)

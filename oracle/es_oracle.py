@@ -74,6 +74,8 @@ def lib():
         _lib.oracle_es_grid_f32_omp.argtypes = [i64, i32, P, P, P, P, i32,
                                                 i32, f32, f32, P]
         _lib.oracle_es_grid_f32_omp.restype = i32
+        _lib.oracle_set_threads.argtypes = [i32]
+        _lib.oracle_set_threads.restype = i32
         _lib.oracle_es_grid_f32_par.argtypes = \
             _lib.oracle_es_grid_f32.argtypes
         _lib.oracle_es_grid_f32_par.restype = i32

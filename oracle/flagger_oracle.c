@@ -27,6 +27,9 @@
  * t == 0, where the reference discards the value).
  */
 #include <complex.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -191,6 +194,19 @@ void oracle_flagger(const void* vis, int is_double, int32_t* flags,
 {
     flagger(vis, is_double, flags, alpha, thr_mag, thr_var, thr_bb, step,
             window, wmh, T, B, C, P);
+}
+
+/* Threads of the OpenMP loop (the bench's CPU baseline sets the job's CPU
+ * share); returns the count in effect. */
+int oracle_flagger_set_threads(int n)
+{
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
 }
 
 /* |v| as the reference computes it (glibc cabsf / cabs), for tests of the

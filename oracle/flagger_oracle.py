@@ -45,6 +45,8 @@ def lib():
         _lib.oracle_flagger.argtypes = [P, i32, P, f64, f64, f64, f64, i32,
                                         i32, i32, i64, i64, i32, i32]
         _lib.oracle_flagger.restype = None
+        _lib.oracle_flagger_set_threads.argtypes = [i32]
+        _lib.oracle_flagger_set_threads.restype = i32
         _lib.oracle_cabs_f32.argtypes = [P, i64, P]
         _lib.oracle_cabs_f64.argtypes = [P, i64, P]
     return _lib

@@ -65,8 +65,10 @@ struct BucketScratch
     size_t table_entries = 0;
 };
 
-// Number of visibility chunks used for a given visibility count.
-int num_chunks(int64_t num_vis);
+// Number of visibility chunks used for a given visibility count and bin
+// count (the chunk-by-bin count table stays below 2^31 bytes, the range of
+// the buffer addressing in k_scan_columns).
+int num_chunks(int64_t num_vis, int nbins);
 
 // Bucketing, fully asynchronous: fills scratch.recs (sized by the caller
 // for the worst case, 4 entries per visibility) and the work-item table;

@@ -769,212 +769,6 @@ __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
     }
 }
 
-// Grid mode, f32, matrix-core form (the hot path).
-//
-// A tile's grid is a sum of rank-1 outer products,
-//   grid[u][v] += sum_k (s_u ku_k[u]) * (s_v kv_k[v] w_k V_k)
-// (s_u s_v = (-1)^(u+v) checkerboard, separable), i.e. C += A B with
-// A[u][k] = taps along u of entry k and B[k][v] = taps along v times the
-// weighted visibility. A workgroup of 16 waves owns a 64x64 tile; wave w
-// keeps the 16x16 sub-tile (w>>2, w&3) in 2 x 4 accumulator registers
-// (re / im) and applies FOUR entries per v_mfma_f32_16x16x4_f32: lane l
-// evaluates A[l&15][l>>4] and B[l>>4][l&15], i.e. one u-tap and one v-tap,
-// with exactly the reference's tap arithmetic. No LDS atomics, no
-// per-cell read-modify-write: the sub-tile leaves the registers once.
-// Entries are staged in LDS 1024 at a time; each wave scans them 64 at a
-// time (ballot of entries whose taps overlap its sub-tile) and walks the
-// set bits four at a time on the scalar unit.
-// Staging of one chunk of bucketed entries into per-sub-tile visit lists
-// (a pool in LDS): thread t classifies entry t by the sub-tiles (a
-// kSub x kSub grid of 16x16 cells starting at the tile origin) its taps
-// touch, counts with one ballot per sub-tile, and after a prefix over the
-// counts writes the entry's 16-byte record once per sub-tile it touches.
-template<int kSub>
-struct VisitPool
-{
-    uint32_t count[kSub * kSub];
-    uint32_t offset[kSub * kSub + 1];
-};
-
-template<int kSub>
-__device__ __forceinline__ void pool_classify(VisitPool<kSub>& vp, int lane,
-        int wlo_r, int whi_r, int wlo_c, int whi_c, int pos[4], int sub[4])
-{
-    int nh = 0;
-#pragma unroll
-    for (int st = 0; st < kSub * kSub; ++st)
-    {
-        const int sr = st / kSub, sc = st % kSub;
-        const bool hit = sr >= wlo_r && sr <= whi_r && sc >= wlo_c &&
-                sc <= whi_c;
-        const uint64_t m = __ballot(hit);
-        if (!m) continue;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&vp.count[st], (uint32_t)__popcll(m));
-        base = __shfl(base, 0);
-        if (hit && nh < 4)
-        {
-            pos[nh] = (int)(base + __popcll(m & ((1ull << lane) - 1ull)));
-            sub[nh] = st;
-            ++nh;
-        }
-    }
-    for (int k = nh; k < 4; ++k) sub[k] = -1;
-}
-
-template<int kSub>
-__device__ __forceinline__ void pool_prefix(VisitPool<kSub>& vp)
-{
-    if (threadIdx.x == 0)
-    {
-        uint32_t run = 0;
-        for (int st = 0; st < kSub * kSub; ++st)
-        {
-            vp.offset[st] = run;
-            run += vp.count[st];
-        }
-        vp.offset[kSub * kSub] = run;
-    }
-}
-
-template<bool DO_W>
-__global__ __launch_bounds__(256) void k_scatter_mfma(EsParams<float> p,
-        const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
-        const uint32_t* __restrict__ item_start,
-        const uint32_t* __restrict__ item_bin, float* __restrict__ grid)
-{
-    using f32x4 = __attribute__((ext_vector_type(4))) float;
-    constexpr int kChunk = 256;           // one entry per thread
-    constexpr int kVec = DO_W ? 2 : 1;    // float4s per bucketed record
-    __shared__ float4 s_pool[4 * kChunk]; // {pu, pv, vre, vim} per visit
-    __shared__ VisitPool<4> s_vp;
-
-    const uint32_t item = blockIdx.x;
-    if (item_bin[item] == kNoBin) return;   // past the last work item
-    const int b = (int)item_bin[item];
-    const uint32_t piece = item - item_start[b];
-    const uint32_t npieces = item_start[b + 1] - item_start[b];
-    const uint32_t e0 = bin_start[b] + piece * kPiece;
-    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
-    const int half = p.G / 2;
-    int r0, c0;
-    tile_origin(p, b, r0, c0);
-    if (r0 >= p.G || c0 >= p.G) return;    // phantom tile
-    const int tu0 = r0 - half, tv0 = c0 - half;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int i = lane & 15, kq = lane >> 4;
-    // This wave owns sub-tiles {wave, wave+4, wave+8, wave+12}: sub-tile
-    // row band (wave) and all four column blocks -> shared A row index.
-    const int sub_r = wave * 16;
-    const int my_u = tu0 + sub_r + i;     // A row: grid u of this lane
-    const float fu = (float)my_u;
-    const float sgn_u = (my_u & 1) ? -1.0f : 1.0f;
-    const float hs = (float)p.support / 2.0f;
-    const float inv_hs = 1.0f / hs;
-    f32x4 acc_re[4], acc_im[4];
-#pragma unroll
-    for (int cblk = 0; cblk < 4; ++cblk)
-    {
-        acc_re[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        acc_im[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    }
-    const float4* recs4 = (const float4*)recs;
-
-    for (uint32_t cb = e0; cb < e1; cb += kChunk)
-    {
-        const int n = (int)min((uint32_t)kChunk, e1 - cb);
-        const int t = threadIdx.x;
-        __syncthreads();   // previous chunk consumed
-        if (t < 16) s_vp.count[t] = 0;
-        float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        int wlo_r = 1, whi_r = 0, wlo_c = 1, whi_c = 0;
-        if (t < n)
-        {
-            r = recs4[(size_t)(cb + t) * kVec];
-            if (DO_W)
-            {
-                const float kw = recs4[(size_t)(cb + t) * kVec + 1].x;
-                r.z *= kw;
-                r.w *= kw;
-            }
-            int u0, u1, v0, v1;
-            tap_range(p, r.x, r.y, u0, u1, v0, v1);
-            wlo_r = max(u0 - tu0, 0) >> 4;
-            whi_r = min(u1 - tu0, kTile - 1) >> 4;
-            wlo_c = max(v0 - tv0, 0) >> 4;
-            whi_c = min(v1 - tv0, kTile - 1) >> 4;
-        }
-        __syncthreads();   // counters zeroed
-        int pos[4], sub[4];
-        pool_classify<4>(s_vp, lane, wlo_r, whi_r, wlo_c, whi_c, pos, sub);
-        __syncthreads();   // counts final
-        pool_prefix<4>(s_vp);
-        __syncthreads();   // offsets final
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (sub[k] >= 0) s_pool[s_vp.offset[sub[k]] + pos[k]] = r;
-        __syncthreads();   // pool complete
-#pragma unroll
-        for (int cblk = 0; cblk < 4; ++cblk)
-        {
-            const int st = wave * 4 + cblk;
-            const int v_beg = __builtin_amdgcn_readfirstlane(
-                    (int)s_vp.offset[st]);
-            const int cnt = __builtin_amdgcn_readfirstlane((int)s_vp.count[st]);
-            const int my_v = tv0 + cblk * 16 + i;   // B col of this lane
-            const float fv = (float)my_v;
-            const float sgn_v = (my_v & 1) ? -1.0f : 1.0f;
-            for (int g = 0; g < cnt; g += 4)
-            {
-#pragma clang fp contract(off)
-                const int slot = g + kq;
-                const bool valid = slot < cnt;
-                const float4 q = s_pool[v_beg + (valid ? slot : cnt - 1)];
-                // Tap u lies in [ceil(pu - W/2), floor(pu + W/2)]
-                // (kernels.cu:332-335) iff pu - W/2 <= u <= pu + W/2.
-                const bool in_u = valid && q.x - hs <= fu && fu <= q.x + hs;
-                const bool in_v = valid && q.y - hs <= fv && fv <= q.y + hs;
-                const float ka = es_tap_fast(p.beta, (fu - q.x) * inv_hs);
-                const float kb = es_tap_fast(p.beta, (fv - q.y) * inv_hs);
-                const float a = in_u ? sgn_u * ka : 0.0f;
-                const float kv = in_v ? sgn_v * kb : 0.0f;
-                const float bre = kv * q.z, bim = kv * q.w;
-                acc_re[cblk] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bre,
-                        acc_re[cblk], 0, 0, 0);
-                acc_im[cblk] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bim,
-                        acc_im[cblk], 0, 0, 0);
-            }
-        }
-    }
-
-    // C/D layout of 16x16x4 f32: col = lane & 15, row = (lane >> 4)*4 + r.
-#pragma unroll
-    for (int cblk = 0; cblk < 4; ++cblk)
-    {
-        const int col = c0 + cblk * 16 + i;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-        {
-            const int row = r0 + sub_r + kq * 4 + r;
-            if (row >= p.G || col >= p.G) continue;
-            float* dst = grid + ((size_t)row * p.G + col) * 2;
-            if (npieces == 1)
-            {
-                float2 v;
-                v.x = acc_re[cblk][r];
-                v.y = acc_im[cblk][r];
-                *(float2*)dst = v;
-            }
-            else
-            {
-                if (acc_re[cblk][r] != 0.0f) unsafeAtomicAdd(dst, acc_re[cblk][r]);
-                if (acc_im[cblk][r] != 0.0f)
-                    unsafeAtomicAdd(dst + 1, acc_im[cblk][r]);
-            }
-        }
-    }
-}
-
 // Atomic-free visit pool of one chunk (tap-table kernels). Phase 1, before
 // a barrier: each wave ballots its entries per sub-tile, keeps for every
 // hit the entry's rank inside the ballot, and lane st publishes the wave's
@@ -1043,13 +837,13 @@ __device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
 }
 
 // Grid mode, f32, matrix-core form with per-entry tap tables (the hot path
-// for W <= 16). Same tile / sub-tile / accumulator organisation as
-// k_scatter_mfma, but the ES taps are evaluated ONCE per bucketed entry
-// instead of once per (entry, sub-tile) visit and lane: at staging, thread
-// t evaluates the NTAP u-taps (checkerboard sign folded in) and the NTAP
-// v-taps times the weighted visibility of its entry into LDS tables
-// (identical arithmetic to k_scatter_mfma, so the products fed to the
-// matrix core are bit-identical). A visit is a packed 32-bit
+// for W <= 16). A 64 x 64 tile per work item, 16 x 16 sub-tiles, four
+// waves of 16-row bands each holding four sub-tiles' re / im in MFMA
+// accumulators: the tile's update is a sum of rank-1 outer products
+// ku (x) (kv w V), applied four visibilities per v_mfma_f32_16x16x4_f32.
+// The ES taps are evaluated ONCE per bucketed entry: at staging, thread t
+// evaluates the NTAP u-taps (checkerboard sign folded in) and the NTAP
+// v-taps times the weighted visibility of its entry into LDS tables. A visit is a packed 32-bit
 // {entry, u0 - tile row + 32, v0 - tile col + 32} word. Per chunk: the
 // next chunk's records are prefetched, the pool is laid out without
 // atomics (pool_count / pool_layout), three barriers, and the MFMA loop
@@ -1298,7 +1092,8 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     }
 }
 
-// Degrid mode, f32, matrix-core form (the hot path).
+// Degrid mode, f32, matrix-core form with per-entry tap tables (the hot
+// path for W <= 16).
 //
 // For visibility j and a 16x16 sub-tile (rows R, cols C) of the grid,
 //   partial_j = sum_r s_u ku_j[r] * (sum_c G[r][c] s_v kv_j[c])
@@ -1314,154 +1109,10 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
 // of one visibility from several sub-tiles meet in an LDS accumulator
 // (16-lane ds_add_f32), and each visibility is read-modify-written in HBM
 // once.
-template<bool DO_W>
-__global__ __launch_bounds__(256) void k_gather_mfma(EsParams<float> p,
-        const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
-        const uint32_t* __restrict__ item_start,
-        const uint32_t* __restrict__ item_bin, const float* __restrict__ grid,
-        float* __restrict__ vis)
-{
-    using f32x4 = __attribute__((ext_vector_type(4))) float;
-    constexpr int kChunk = 256;
-    constexpr int kSub = 5;                 // 5 x 5 sub-tiles: tile + halo
-    __shared__ float4 s_pool[4 * kChunk];   // {pu, pv, kw*flip, e} per visit
-    __shared__ float s_acc_re[kChunk];
-    __shared__ float s_acc_im[kChunk];
-    __shared__ VisitPool<kSub> s_vp;
-
-    const uint32_t item = blockIdx.x;
-    if (item_bin[item] == kNoBin) return;   // past the last work item
-    const int b = (int)item_bin[item];
-    const uint32_t piece = item - item_start[b];
-    const uint32_t e0 = bin_start[b] + piece * kPiece;
-    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
-    if (e0 >= e1) return;   // empty tile
-    const int half = p.G / 2;
-    int r0, c0;
-    tile_origin(p, b, r0, c0);
-    if (r0 >= p.G || c0 >= p.G) return;    // phantom tile
-    const int tu0 = r0 - half, tv0 = c0 - half;
-    const float2* g2 = (const float2*)grid;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int jl = lane & 15, kq = lane >> 4;
-    const float hs = (float)p.support / 2.0f;
-    const float inv_hs = 1.0f / hs;
-    const float4* recs4 = (const float4*)recs;
-
-    for (uint32_t cb = e0; cb < e1; cb += kChunk)
-    {
-        const int n = (int)min((uint32_t)kChunk, e1 - cb);
-        const int t = threadIdx.x;
-        __syncthreads();   // previous chunk consumed
-        if (t < kSub * kSub) s_vp.count[t] = 0;
-        float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        int wlo_r = 1, whi_r = 0, wlo_c = 1, whi_c = 0;
-        if (t < n)
-        {
-            r = recs4[cb + t];
-            int u0, u1, v0, v1;
-            tap_range(p, r.x, r.y, u0, u1, v0, v1);
-            wlo_r = (u0 - tu0) >> 4;
-            whi_r = min(u1 - tu0, kSub * 16 - 1) >> 4;
-            wlo_c = (v0 - tv0) >> 4;
-            whi_c = min(v1 - tv0, kSub * 16 - 1) >> 4;
-        }
-        s_acc_re[t] = 0.0f;
-        s_acc_im[t] = 0.0f;
-        __syncthreads();
-        int pos[4], sub[4];
-        pool_classify<kSub>(s_vp, lane, wlo_r, whi_r, wlo_c, whi_c, pos, sub);
-        __syncthreads();
-        pool_prefix<kSub>(s_vp);
-        __syncthreads();
-        const float4 q_mine = make_float4(r.x, r.y, r.z, __int_as_float(t));
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (sub[k] >= 0) s_pool[s_vp.offset[sub[k]] + pos[k]] = q_mine;
-        __syncthreads();
-        for (int st = wave; st < kSub * kSub; st += 4)
-        {
-            const int cnt = __builtin_amdgcn_readfirstlane((int)s_vp.count[st]);
-            if (cnt == 0) continue;
-            const int v_beg = __builtin_amdgcn_readfirstlane(
-                    (int)s_vp.offset[st]);
-            const int R0 = (st / kSub) * 16, C0 = (st % kSub) * 16;
-            // A operands straight from the grid (L2 / HBM):
-            // G[r0 + R0 + jl][c0 + C0 + 4 kk + kq], kk = 0..3.
-            float a_re[4], a_im[4];
-            const int grow = r0 + R0 + jl;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-            {
-                const int gcol = c0 + C0 + 4 * kk + kq;
-                float2 v = make_float2(0.0f, 0.0f);
-                if (grow < p.G && gcol < p.G) v = g2[(size_t)grow * p.G + gcol];
-                a_re[kk] = v.x;
-                a_im[kk] = v.y;
-            }
-            for (int g = 0; g < cnt; g += 16)
-            {
-#pragma clang fp contract(off)
-                const bool valid = g + jl < cnt;
-                const float4 q = s_pool[v_beg + (valid ? g + jl : cnt - 1)];
-                f32x4 t_re = {0.0f, 0.0f, 0.0f, 0.0f};
-                f32x4 t_im = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk)
-                {
-                    const int v = tv0 + C0 + 4 * kk + kq;
-                    const float fv = (float)v;
-                    const bool in_v = valid && q.y - hs <= fv && fv <= q.y + hs;
-                    const float k = es_tap_fast(p.beta, (fv - q.y) * inv_hs);
-                    const float kv = in_v ? ((v & 1) ? -k : k) : 0.0f;
-                    t_re = __builtin_amdgcn_mfma_f32_16x16x4f32(a_re[kk], kv,
-                            t_re, 0, 0, 0);
-                    t_im = __builtin_amdgcn_mfma_f32_16x16x4f32(a_im[kk], kv,
-                            t_im, 0, 0, 0);
-                }
-                float p_re = 0.0f, p_im = 0.0f;
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr)
-                {
-                    const int u = tu0 + R0 + 4 * kq + rr;
-                    const float fu = (float)u;
-                    const bool in_u = valid && q.x - hs <= fu && fu <= q.x + hs;
-                    const float k = es_tap_fast(p.beta, (fu - q.x) * inv_hs);
-                    const float ku = in_u ? ((u & 1) ? -k : k) : 0.0f;
-                    p_re += ku * t_re[rr];
-                    p_im += ku * t_im[rr];
-                }
-                // Sum the four lane groups (rows 4kq..4kq+3).
-                p_re = sdp_hip::sum_rows16(p_re);
-                p_im = sdp_hip::sum_rows16(p_im);
-                if (kq == 0 && valid)
-                {
-                    const int e = __float_as_int(q.w);
-                    const float kw = DO_W ? fabsf(q.z) : 1.0f;
-                    atomicAdd(&s_acc_re[e], p_re * kw);
-                    atomicAdd(&s_acc_im[e], p_im * kw);
-                }
-            }
-        }
-        __syncthreads();
-        if (t < n)
-        {
-            const uint64_t idx = (uint64_t)__float_as_uint(r.w);
-            const float flip = signbit(r.z) ? -1.0f : 1.0f;
-            vis[2 * idx] += s_acc_re[t];
-            vis[2 * idx + 1] += s_acc_im[t] * flip;   // kernels.cu:267-268
-        }
-    }
-}
-
-// Degrid mode, f32, matrix-core form with per-entry tap tables (the hot
-// path for W <= 16). Same organisation as k_gather_mfma (5 x 5 sub-tiles
-// of a tile + halo, T = G_sub * Kv on the matrix core, u-taps applied on
-// the lane-group reduction), but each entry's NTAP u-taps and v-taps
-// (checkerboard sign folded in) are evaluated once at staging into LDS
-// tables, with the same arithmetic as k_gather_mfma; visits are packed
-// {entry, u0 - tile row, v0 - tile col} words; the pool is laid out
-// without atomics and the next chunk's records are prefetched.
+// Each entry's NTAP u-taps and v-taps (checkerboard sign folded in) are
+// evaluated once at staging into LDS tables; visits are packed {entry,
+// u0 - tile row, v0 - tile col} words; the pool is laid out without atomics
+// and the next chunk's records are prefetched.
 template<bool DO_W, int NTAP>
 __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
@@ -1995,11 +1646,14 @@ int bucket_threads()
     return v;
 }
 
-int num_chunks(int64_t num_vis)
+int num_chunks(int64_t num_vis, int nbins)
 {
     const int64_t cv = chunk_vis();
     const int64_t by_size = (num_vis + cv - 1) / cv;
-    return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxChunks, by_size));
+    const int64_t by_table = (((int64_t)1 << 31) - 1) /
+            (4 * (int64_t)std::max(1, nbins));
+    return (int)std::max<int64_t>(1, std::min<int64_t>(
+            std::min<int64_t>(kMaxChunks, by_table), by_size));
 }
 
 template<typename T, int MODE, int NT>
@@ -2038,7 +1692,7 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
     sdp_Error st = SDP_SUCCESS;
     sdp_Error* status = &st;
     const int64_t num_vis = num_rows * num_chan;
-    const int nc = num_chunks(num_vis);
+    const int nc = num_chunks(num_vis, p.nbins);
     const int64_t chunk = (num_rows + nc - 1) / nc;   // rows per chunk
     const int passes = (p.nbins + kBinsPerPass - 1) / kBinsPerPass;
     const dim3 grid_b(nc, passes);
@@ -2092,17 +1746,6 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
     return *status;
 }
 
-// Tap-table tile kernels (k_scatter_tab / k_gather_tab) unless
-// SDP_ES_TAP_TABLES=0 selects the per-visit tap kernels (A/B measurement).
-bool use_tap_tables()
-{
-    static const bool on = [] {
-        const char* e = std::getenv("SDP_ES_TAP_TABLES");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 template<typename T>
 int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         T* grid, hipStream_t stream, bool skip_empty)
@@ -2112,37 +1755,34 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
             p, s.item_start, grid);
     SDP_HIP_CHECK_LAUNCH(status);
+    // f32: the matrix-core tile kernels with per-entry tap tables (float
+    // plans have W <= 16, sdp_gridder_uvw_es_fft_utils.cpp:498); f64 (and
+    // any wider float support): LDS accumulation below.
     if constexpr (sizeof(T) == 4)
     {
         const float* recs = (const float*)s.recs;
-        if (!use_tap_tables())
-            ;
-        else if (p.support <= 8 && p.do_w)
-            k_scatter_tab<true, 9><<<n_items, 256, 0, stream>>>(
-                    p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                    skip_empty ? 1 : 0);
-        else if (p.support <= 8)
-            k_scatter_tab<false, 9><<<n_items, 256, 0, stream>>>(
-                    p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                    skip_empty ? 1 : 0);
-        else if (p.support <= 16 && p.do_w)
-            k_scatter_tab<true, 17><<<n_items, 256, 0, stream>>>(
-                    p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                    skip_empty ? 1 : 0);
-        else if (p.support <= 16)
-            k_scatter_tab<false, 17><<<n_items, 256, 0, stream>>>(
-                    p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                    skip_empty ? 1 : 0);
-        if (use_tap_tables() && p.support <= 16)
-            ;
-        else if (p.do_w)
-            k_scatter_mfma<true><<<n_items, 256, 0, stream>>>(
-                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
-        else
-            k_scatter_mfma<false><<<n_items, 256, 0, stream>>>(
-                    p, recs, s.bin_start, s.item_start, s.item_bin, grid);
-        SDP_HIP_CHECK_LAUNCH(status);
-        return *status;
+        const int se = skip_empty ? 1 : 0;
+        if (p.support <= 16)
+        {
+            if (p.support <= 8 && p.do_w)
+                k_scatter_tab<true, 9><<<n_items, 256, 0, stream>>>(
+                        p, recs, s.bin_start, s.item_start, s.item_bin, grid,
+                        se);
+            else if (p.support <= 8)
+                k_scatter_tab<false, 9><<<n_items, 256, 0, stream>>>(
+                        p, recs, s.bin_start, s.item_start, s.item_bin, grid,
+                        se);
+            else if (p.do_w)
+                k_scatter_tab<true, 17><<<n_items, 256, 0, stream>>>(
+                        p, recs, s.bin_start, s.item_start, s.item_bin, grid,
+                        se);
+            else
+                k_scatter_tab<false, 17><<<n_items, 256, 0, stream>>>(
+                        p, recs, s.bin_start, s.item_start, s.item_bin, grid,
+                        se);
+            SDP_HIP_CHECK_LAUNCH(status);
+            return *status;
+        }
     }
     const size_t lds = 2 * (size_t)kTile * kScatterStride * sizeof(T);
     if (p.do_w)
@@ -2183,41 +1823,27 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     if constexpr (sizeof(T) == 4)
     {
         const float* recs = (const float*)s.recs;
-        if (use_tap_tables() && p.support <= 8 && sort_pieces())
-        {
-            k_sort_pieces<<<n_items, 256, 0, stream>>>(p,
-                    (float*)s.recs, s.bin_start, s.item_start, s.item_bin);
-            SDP_HIP_CHECK_LAUNCH(status);
-        }
-        if (!use_tap_tables())
-            ;
-        else if (p.support <= 8 && p.do_w)
-            k_gather_tab<true, 9><<<n_items, 256, 0, stream>>>(p, recs,
-                    s.bin_start, s.item_start, s.item_bin, grid, vis);
-        else if (p.support <= 8)
-            k_gather_tab<false, 9><<<n_items, 256, 0, stream>>>(p, recs,
-                    s.bin_start, s.item_start, s.item_bin, grid, vis);
-        else if (p.support <= 16 && p.do_w)
-            k_gather_tab<true, 17><<<n_items, 256, 0, stream>>>(p, recs,
-                    s.bin_start, s.item_start, s.item_bin, grid, vis);
-        else if (p.support <= 16)
-            k_gather_tab<false, 17><<<n_items, 256, 0, stream>>>(p, recs,
-                    s.bin_start, s.item_start, s.item_bin, grid, vis);
-        if (p.support <= 16 && use_tap_tables())
-        {
-            SDP_HIP_CHECK_LAUNCH(status);
-            return *status;
-        }
         if (p.support <= 16)
         {
-            if (p.do_w)
-                k_gather_mfma<true><<<n_items, 256, 0, stream>>>(
-                        p, (const float*)s.recs, s.bin_start, s.item_start,
-                        s.item_bin, grid, vis);
+            if (p.support <= 8 && sort_pieces())
+            {
+                k_sort_pieces<<<n_items, 256, 0, stream>>>(p,
+                        (float*)s.recs, s.bin_start, s.item_start,
+                        s.item_bin);
+                SDP_HIP_CHECK_LAUNCH(status);
+            }
+            if (p.support <= 8 && p.do_w)
+                k_gather_tab<true, 9><<<n_items, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis);
+            else if (p.support <= 8)
+                k_gather_tab<false, 9><<<n_items, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis);
+            else if (p.do_w)
+                k_gather_tab<true, 17><<<n_items, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis);
             else
-                k_gather_mfma<false><<<n_items, 256, 0, stream>>>(
-                        p, (const float*)s.recs, s.bin_start, s.item_start,
-                        s.item_bin, grid, vis);
+                k_gather_tab<false, 17><<<n_items, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis);
             SDP_HIP_CHECK_LAUNCH(status);
             return *status;
         }

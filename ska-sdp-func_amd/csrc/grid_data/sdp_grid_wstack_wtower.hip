@@ -1689,18 +1689,28 @@ enum BufId
 
 std::mutex g_mutex;                  // one driver call at a time
 
+// The HIP device of the calling thread: every cache below is per device
+// (a process may drive several GPUs; device buffers and plans of one are
+// not usable on another).
+int current_device()
+{
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return dev;
+}
+
 Workspace& workspace()
 {
-    static Workspace ws;
-    return ws;
+    static std::map<int, Workspace> ws;
+    return ws[current_device()];
 }
 
 sdp_fft::Plan2D* cached_plan(int n, bool dbl, size_t batch, size_t dist,
         sdp_Error* status)
 {
-    static std::map<std::tuple<int, bool, size_t, size_t>,
+    static std::map<std::tuple<int, int, bool, size_t, size_t>,
             sdp_fft::Plan2D*> cache;
-    const auto key = std::make_tuple(n, dbl, batch, dist);
+    const auto key = std::make_tuple(current_device(), n, dbl, batch, dist);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
     sdp_fft::Plan2D* p = sdp_fft::create_2d_batched(n, n, dbl, batch, dist,
@@ -1723,8 +1733,9 @@ const sdp_es::FftTwiddles* plane_fft_twiddles(int64_t G, bool dbl,
     }
     if (!use || dbl || G > INT32_MAX || !sdp_es::fused_fft_supported((int)G))
         return nullptr;
-    static std::map<int64_t, sdp_es::FftTwiddles> cache;
-    auto it = cache.find(G);
+    static std::map<std::pair<int, int64_t>, sdp_es::FftTwiddles> cache;
+    const auto key = std::make_pair(current_device(), G);
+    auto it = cache.find(key);
     if (it != cache.end()) return &it->second;
     sdp_es::FftTwiddles tw;
     if (sdp_es::fft_twiddles_create((int)G, &tw) != 0)
@@ -1732,17 +1743,17 @@ const sdp_es::FftTwiddles* plane_fft_twiddles(int64_t G, bool dbl,
         *status = SDP_ERR_RUNTIME;
         return nullptr;
     }
-    return &(cache[G] = tw);
+    return &(cache[key] = tw);
 }
 
 sdp_GridderWtowerUVW* cached_kernel(int image_size, int S, double theta,
         double w_step, double hu, double hv, int support, int os,
         int w_support, int wos, sdp_Error* status)
 {
-    static std::map<std::tuple<int, int, double, double, double, double, int,
-            int, int, int>, sdp_GridderWtowerUVW*> cache;
-    const auto key = std::make_tuple(image_size, S, theta, w_step, hu, hv,
-            support, os, w_support, wos);
+    static std::map<std::tuple<int, int, int, double, double, double,
+            double, int, int, int, int>, sdp_GridderWtowerUVW*> cache;
+    const auto key = std::make_tuple(current_device(), image_size, S, theta,
+            w_step, hu, hv, support, os, w_support, wos);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
     sdp_GridderWtowerUVW* k = sdp_gridder_wtower_uvw_create(image_size, S,
@@ -2383,9 +2394,16 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
             }
         }
         // Sub-grids into the grid.
-        // Sub-grids covering a cell per axis: ceil(S / eff), plus one
-        // through the periodic wrap.
-        const int ncand = (g.S + g.eff - 1) / g.eff + 1;
+        // Sub-grids covering a cell per axis: ceil(S / eff) per periodic
+        // image of the cell (x - G, x, x + G) that falls inside the axis'
+        // sub-grid span L = (n - 1) eff + S; at most floor(L / G) + 1 of
+        // the three do (a uvw extent wider than the grid wraps onto it).
+        auto axis_cand = [&](int64_t n_idx) {
+            const int64_t L = (n_idx - 1) * g.eff + g.S;
+            const int64_t wraps = std::min<int64_t>(3, L / G + 1);
+            return (int)(((g.S + g.eff - 1) / g.eff) * wraps);
+        };
+        const int ncand = std::max(axis_cand(g.nu), axis_cand(g.nv));
         if (ncand <= 3)
             k_gather_grid<T, 3><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
                     d_grid, G, d_stack, g.S, d_slot_of + gi * g.ntask, g.nu,

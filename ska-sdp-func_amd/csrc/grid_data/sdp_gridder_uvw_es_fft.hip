@@ -217,7 +217,7 @@ void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
         SDP_HIP_CHECK(hipMalloc(&s.recs, rec_bytes), status);
         s.recs_bytes = *status ? 0 : rec_bytes;
     }
-    const size_t need = (size_t)sdp_es::num_chunks(num_vis) * plan->nbins;
+    const size_t need = (size_t)sdp_es::num_chunks(num_vis, plan->nbins) * plan->nbins;
     if (need > s.table_entries)
     {
         if (s.table) SDP_HIP_CHECK(hipFree(s.table), status);

@@ -244,3 +244,31 @@ def test_fused_towers_match_double_precision(device, degrid):
         # Interior only: the grid correction amplifies f32 rounding near
         # the facet edge (module docstring).
         _close(im32.cpu().numpy(), im64.cpu().numpy(), 5e-5, border=N // 4)
+
+
+@pytest.mark.parametrize("uv_frac", [0.75, 1.3])
+def test_uv_extent_wider_than_grid(device, uv_frac):
+    """Sub-grids past the grid edge wrap onto it (subgrid_add / cut_out use
+    periodic indices, sdp_gridder_utils.cpp:553-648): a cell can then be
+    covered by sub-grids from two or three periodic images; every one of
+    them must be summed (gridding) and read (degridding) as the oracle's
+    task-by-task restatement does."""
+    import ska_sdp_func.grid_data as g
+    c = wd.wstack_case(num_rows=600, num_chan=2, seed=9, uv_frac=uv_frac)
+    N, S = 256, 64
+    rng = np.random.default_rng(10)
+    vis = (rng.normal(size=(600, 2)) + 1j * rng.normal(size=(600, 2)))
+    a = (c["f0"], c["df"], c["uvw"]) + _args(c, S)[3:]
+    ref = wo.wstack_grid_all(vis, *a, np.zeros((N, N), np.complex128))
+    out = np.zeros((N, N), np.complex128)
+    g.wstack_wtower_grid_all(vis, a[0], a[1], c["uvw"], *a[3:], 0, out)
+    _close(out, ref, 2e-9, border=32)
+    img = _image(N, rng)
+    img[:16] = 0
+    img[-16:] = 0
+    img[:, :16] = 0
+    img[:, -16:] = 0
+    vref = wo.wstack_degrid_all(img, *a, np.zeros((600, 2), complex))
+    v = np.zeros((600, 2), np.complex128)
+    g.wstack_wtower_degrid_all(img, a[0], a[1], c["uvw"], *a[3:], 0, v)
+    _close(v, vref, 2e-9)

@@ -74,13 +74,14 @@ def ref_image(subgrid_size=64):
 
 
 def wstack_case(num_rows=1000, num_chan=3, image_size=256, theta=0.01,
-                fov=0.008, w_tower_height=4.0, w_planes=3.0, seed=0):
-    """uvw [m] in a disk covering 80 % of the grid and w over
+                fov=0.008, w_tower_height=4.0, w_planes=3.0, seed=0,
+                uv_frac=0.4):
+    """uvw [m] in a disk covering 2 uv_frac of the grid (80 %) and w over
     +-w_planes w-stack planes; f0 = c (1 m wavelength), df = c / 200."""
     from oracle import wtower_oracle as wo
     rng = np.random.default_rng(seed)
     w_step = wo.determine_w_step(theta, fov, 0.0, 0.0)
-    rmax = 0.4 * image_size / theta / (1 + (num_chan - 1) / 200.0)
+    rmax = uv_frac * image_size / theta / (1 + (num_chan - 1) / 200.0)
     r = rmax * np.sqrt(rng.random(num_rows))
     ph = rng.random(num_rows) * 2 * np.pi
     wmax = w_planes * w_tower_height * w_step
