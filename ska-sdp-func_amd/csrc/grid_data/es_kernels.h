@@ -27,6 +27,8 @@ constexpr int kCoarseTile = kTile * kCoarse;   // 256 cells
 constexpr int kBinsPerPass = 16384;    // LDS histogram capacity (64 KiB)
 constexpr int kPiece = 4096;           // max entries per scatter work item
 constexpr int kMaxChunks = 1024;       // chunks of visibilities per bucketing
+constexpr int kTapPolyPairs = 3;       // interior taps 1..6 of W = 8
+constexpr int kTapPolyDeg = 10;        // ~1e-9 relative (f32 Horner ~5e-7)
 
 enum Mode { MODE_GRID = 0, MODE_DEGRID = 1 };
 
@@ -48,7 +50,18 @@ struct EsParams
     T uv_scale;         // G * pixel_size
     T w_scale;
     T min_plane_w;
+    // f32 tile kernels at W = 8: interior taps d = 1..6 as polynomials of
+    // s = 2 delta - 1 (delta = first tap - (pos - W / 2) in [0, 1)), pairs
+    // (1, 2), (3, 4), (5, 6), coefficient k of both taps of a pair side by
+    // side, (-1)^d folded in (es_tap_poly_fit).
+    float tap_poly[kTapPolyPairs][kTapPolyDeg + 1][2];
+    int tap_poly_ok;    // coefficients valid (f32 plan, W = 8)
 };
+
+// Chebyshev fit (double, nodes of degree kTapPolyDeg) of the interior ES
+// taps of support 8 for the f32 beta, converted to monomials in s.
+void es_tap_poly_fit(double beta_f32, float out[kTapPolyPairs]
+        [kTapPolyDeg + 1][2]);
 
 // Scratch owned by a plan (device pointers).
 struct BucketScratch

@@ -57,6 +57,62 @@ __device__ __forceinline__ float es_tap_fast(float beta, float x)
     return (xx > 1.0f) ? 0.0f : r;
 }
 
+// Taps of one axis of a bucketed entry for the f32 tile kernels: slot d
+// holds the tap at u0 + d (u0 the clamped first tap, zero past u1), with
+// the checkerboard factor (-1)^d of the slot (the entry's (-1)^u0 is
+// applied by the caller). kernels.cu:97-102 evaluates every tap as
+// exp(beta (sqrt(1 - x^2) - 1)); here, for W = 8 and an unclamped first
+// tap, the two edge taps (d = 0, 7: the sqrt branch point makes them
+// non-polynomial) and the exact-integer ninth tap are evaluated that way,
+// and the six interior taps (smooth in delta = u0 - (pos - 4) in [0, 1))
+// as degree-10 polynomials of s = 2 delta - 1 in packed-f32 Horner form,
+// two taps per v_pk_fma_f32 (~5e-7 relative in f32, es_tap_poly_fit):
+// 3 exp/sqrt pairs per axis instead of 9.
+template<int NTAP, bool POLY>
+__device__ __forceinline__ void axis_taps(const EsParams<float>& p, float pos,
+        int u0, int u1, float (&t)[NTAP])
+{
+#pragma clang fp contract(off)
+    using f2 = __attribute__((ext_vector_type(2))) float;
+    const float hs = (float)p.support / 2.0f;
+    const float inv_hs = 1.0f / hs;
+#ifndef SDP_AB_NO_TAP_POLY   // (A/B builds only: scripts/variant_lib.sh)
+    if (POLY && NTAP == 9 && p.tap_poly_ok && u1 >= u0 + 7 &&
+            u0 == (int)ceilf(pos - hs))
+    {
+        const float dl = ((float)u0 - pos) + hs;    // exact, in [0, 1)
+        const float sv = dl * 2.0f - 1.0f;           // exact
+        const f2 s2 = {sv, sv};
+#pragma unroll
+        for (int q = 0; q < kTapPolyPairs; ++q)
+        {
+            f2 y = {p.tap_poly[q][kTapPolyDeg][0], p.tap_poly[q][kTapPolyDeg][1]};
+#pragma unroll
+            for (int k = kTapPolyDeg - 1; k >= 0; --k)
+            {
+                const f2 c = {p.tap_poly[q][k][0], p.tap_poly[q][k][1]};
+                y = __builtin_elementwise_fma(y, s2, c);
+            }
+            t[1 + 2 * q] = y.x;
+            t[2 + 2 * q] = y.y;
+        }
+        t[0] = es_tap_fast(p.beta, ((float)u0 - pos) * inv_hs);
+        t[7] = -es_tap_fast(p.beta, ((float)(u0 + 7) - pos) * inv_hs);
+        t[8] = 0.0f;
+        if (u1 >= u0 + 8)   // exact-integer position: W + 1 taps
+            t[NTAP - 1] = es_tap_fast(p.beta,
+                    ((float)(u0 + 8) - pos) * inv_hs);
+        return;
+    }
+#endif
+#pragma unroll
+    for (int d = 0; d < NTAP; ++d)
+    {
+        const float k = es_tap_fast(p.beta, ((float)(u0 + d) - pos) * inv_hs);
+        t[d] = (u0 + d <= u1) ? ((d & 1) ? -k : k) : 0.0f;
+    }
+}
+
 // Tap range of one visibility on the current w-plane (kernels.cu:150-196,
 // 301-347). Returns false if the visibility does not touch the plane.
 template<typename T>
@@ -890,8 +946,6 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     const int i = lane & 15, kq = lane >> 4;
     const int sub_r = wave * 16;           // this wave's row band
     const int base_u = sub_r + i + 32;     // tap index = base_u - packed ou
-    const float hs = (float)p.support / 2.0f;
-    const float inv_hs = 1.0f / hs;
     f32x4 acc_re[4], acc_im[4];
 #pragma unroll
     for (int cblk = 0; cblk < 4; ++cblk)
@@ -949,18 +1003,18 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         if (t < n)
         {
 #pragma clang fp contract(off)
+            float tu[NTAP], tv[NTAP];
+            axis_taps<NTAP, true>(p, r.x, u0, u1, tu);
+            axis_taps<NTAP, true>(p, r.y, v0, v1, tv);
+            // (-1)^(u0 + v0) of the checkerboard, on the weighted
+            // visibility (sign flips: the products are unchanged)
+            const bool neg = ((u0 + v0) & 1) != 0;
+            const float zr = neg ? -r.z : r.z, zi = neg ? -r.w : r.w;
 #pragma unroll
             for (int d = 0; d < NTAP; ++d)
             {
-                const int u = u0 + d, v = v0 + d;
-                const float ka = es_tap_fast(p.beta, ((float)u - r.x) * inv_hs);
-                const float kb = es_tap_fast(p.beta, ((float)v - r.y) * inv_hs);
-                const float a = (u & 1) ? -ka : ka;
-                const float kv = (v & 1) ? -kb : kb;
-                s_ku[t * NTAP + d] = (u <= u1) ? a : 0.0f;
-                s_kv[t * NTAP + d] = (v <= v1) ?
-                        make_float2(kv * r.z, kv * r.w) :
-                        make_float2(0.0f, 0.0f);
+                s_ku[t * NTAP + d] = tu[d];
+                s_kv[t * NTAP + d] = make_float2(tv[d] * zr, tv[d] * zi);
             }
         }
         __syncthreads();   // B2: entry info and tap tables complete
@@ -1148,8 +1202,6 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     const int jl = lane & 15, kq = lane >> 4;
-    const float hs = (float)p.support / 2.0f;
-    const float inv_hs = 1.0f / hs;
     const float4* recs4 = (const float4*)recs;
     if (t == 0)
     {
@@ -1184,16 +1236,18 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         if (t < n)
         {
 #pragma clang fp contract(off)
+            float tu[NTAP], tv[NTAP];
+            axis_taps<NTAP, false>(p, r.x, u0, u1, tu);
+            axis_taps<NTAP, false>(p, r.y, v0, v1, tv);
 #pragma unroll
             for (int d = 0; d < NTAP; ++d)
             {
-                const int u = u0 + d, v = v0 + d;
-                const float ka = es_tap_fast(p.beta, ((float)u - r.x) * inv_hs);
-                const float kb = es_tap_fast(p.beta, ((float)v - r.y) * inv_hs);
-                s_ku[t * NTAP + d] = (u <= u1) ? ((u & 1) ? -ka : ka) : 0.0f;
-                s_kv[t * NTAP + d] = (v <= v1) ? ((v & 1) ? -kb : kb) : 0.0f;
+                s_ku[t * NTAP + d] = tu[d];
+                s_kv[t * NTAP + d] = tv[d];
             }
-            s_kw[t] = DO_W ? fabsf(r.z) : 1.0f;
+            // (-1)^(u0 + v0) of the checkerboard, with the w-tap
+            const float kw = DO_W ? fabsf(r.z) : 1.0f;
+            s_kw[t] = ((u0 + v0) & 1) ? -kw : kw;
         }
         s_acc_re[t] = 0.0f;
         s_acc_im[t] = 0.0f;
@@ -1621,6 +1675,53 @@ dim3 image_blocks(int n)
 }
 
 } // namespace
+
+void es_tap_poly_fit(double beta, float out[kTapPolyPairs]
+        [kTapPolyDeg + 1][2])
+{
+    // Interior taps d = 1..6 of W = 8 (half support 4):
+    //   psi_d(s) = exp(beta (sqrt(1 - x^2) - 1)), x = ((s + 1) / 2 + d) / 4 - 1
+    // interpolated at the Chebyshev nodes of degree n - 1 in double, then
+    // expanded into monomials of s, with (-1)^d folded in.
+    constexpr int n = kTapPolyDeg + 1;
+    const double pi = 3.14159265358979323846;
+    for (int d = 1; d <= 2 * kTapPolyPairs; ++d)
+    {
+        double f[n], a[n];
+        for (int k = 0; k < n; ++k)
+        {
+            const double sk = cos(pi * (k + 0.5) / n);
+            const double x = ((sk + 1.0) / 2.0 + d) / 4.0 - 1.0;
+            f[k] = exp(beta * (sqrt(1.0 - x * x) - 1.0));
+        }
+        for (int j = 0; j < n; ++j)
+        {
+            double acc = 0.0;
+            for (int k = 0; k < n; ++k)
+                acc += f[k] * cos(pi * j * (k + 0.5) / n);
+            a[j] = acc * 2.0 / n;
+        }
+        a[0] *= 0.5;
+        // sum_j a_j T_j(s) -> monomials, T_{j+1} = 2 s T_j - T_{j-1}.
+        double mono[n] = {0.0}, tm1[n] = {0.0}, t0[n] = {0.0}, t1[n];
+        t0[0] = 1.0;                       // T_0
+        for (int j = 0; j < n; ++j)
+        {
+            for (int k = 0; k < n; ++k) mono[k] += a[j] * t0[k];
+            for (int k = 0; k < n; ++k)
+                t1[k] = (k > 0 ? (j == 0 ? 1.0 : 2.0) * t0[k - 1] : 0.0) -
+                        (j == 0 ? 0.0 : tm1[k]);
+            for (int k = 0; k < n; ++k)
+            {
+                tm1[k] = t0[k];
+                t0[k] = t1[k];
+            }
+        }
+        const double sign = (d & 1) ? -1.0 : 1.0;
+        for (int k = 0; k < n; ++k)
+            out[(d - 1) / 2][k][(d - 1) % 2] = (float)(sign * mono[k]);
+    }
+}
 
 // Visibilities per bucketing chunk (env SDP_ES_CHUNK_VIS for experiments).
 int64_t chunk_vis()

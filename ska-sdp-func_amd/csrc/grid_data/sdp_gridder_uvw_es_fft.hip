@@ -32,6 +32,8 @@ struct sdp_GridderUvwEsFft
     int grid_size;
     int support;
     double beta;          // full beta (table beta * support)
+    float tap_poly[sdp_es::kTapPolyPairs][sdp_es::kTapPolyDeg + 1][2];
+    int tap_poly_ok;      // f32 plan with W = 8: polynomial interior taps
     double pixel_size;
     double uv_scale;
     double min_plane_w;
@@ -266,6 +268,8 @@ sdp_es::EsParams<T> es_params(const sdp_GridderUvwEsFft* plan, int plane)
     p.uv_scale = (T)plan->uv_scale;
     p.w_scale = (T)plan->w_scale;
     p.min_plane_w = (T)plan->min_plane_w;
+    memcpy(p.tap_poly, plan->tap_poly, sizeof(p.tap_poly));
+    p.tap_poly_ok = plan->tap_poly_ok;
     return p;
 }
 
@@ -500,6 +504,13 @@ sdp_GridderUvwEsFft* sdp_gridder_uvw_es_fft_create_plan(
             plan->is_double != 0, &plan->grid_size, &plan->support, &beta_w);
     plan->beta = beta_w * plan->support;
     plan->uv_scale = plan->grid_size * plan->pixel_size;
+    // Interior taps as polynomials (f32 tile kernels, W = 8), fitted to the
+    // beta the f32 kernels use.
+    if (!plan->is_double && plan->support == 8)
+    {
+        sdp_es::es_tap_poly_fit((double)(float)plan->beta, plan->tap_poly);
+        plan->tap_poly_ok = 1;
+    }
 
     // w-plane geometry, sdp_gridder_uvw_es_fft.cpp:346-383.
     if (plan->do_wstacking)
