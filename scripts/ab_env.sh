@@ -7,6 +7,6 @@ for r in $(seq 1 "$ROUNDS"); do
     for v in $VALS; do
         f=${v//\//_}
         env "$VAR=$v" timeout -k 10 200 python3 -u bench.py --no-cpu-baseline "$@" > "$OUT/b_${f}_$r.json" 2> "$OUT/b_${f}_$r.err" || { rc=$?; tail -5 "$OUT/b_${f}_$r.err"; exit $rc; }
-        python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['phases_ms'], d.get('degrid',{}).get('mvis_s'), d.get('degrid',{}).get('phases_ms'))" "$OUT/b_${f}_$r.json" "$VAR=$v"
+        python3 "$(dirname "$0")/ab_summary.py" "$OUT/b_${f}_$r.json" "$VAR=$v"
     done
 done
