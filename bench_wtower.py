@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--degrid", action="store_true")
     ap.add_argument("--verbosity", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-subgrids", type=int, default=6)
+    ap.add_argument("--cpu-task-stride", type=int, default=8)
     return ap.parse_args()
 
 
@@ -87,47 +87,64 @@ def make_inputs(torch, dev, args, w_stack_dist, seed):
 
 
 def cpu_baseline(uvw_dev, vis_dev, args, theta, w_step, H):
-    """Oracle (oracle/wtower_oracle.py, numpy) on a bounded sample: the
-    sub-grid towers (w-towers gridding + sub-grid FFT) of a few sub-grids
-    of the central w-stack plane; the per-plane image FFT / correction are
-    not in the sample."""
+    """C/OpenMP port of the reference CPU grid_all (oracle/wtower_port.c,
+    checked against the numpy restatement by tests/test_wtower_port.py) on
+    a bounded sample of the same inputs, on the job's host-CPU share.
+
+    Sample: the central w-stack plane. Its sub-grid towers are run for
+    every k-th non-empty sub-grid task (k = --cpu-task-stride; each task is
+    one sub-grid tower, the reference's unit of CPU parallelism), then the
+    whole plane's FFT, grid correction and accumulation. The plane time is
+    projected as t_towers * (tasks present / tasks run) + t_plane, and the
+    value is the plane's visibilities over that time. The per-call set-up
+    (kernel tables, PSWF tables, bounds) is not timed.
+    """
     import numpy as np
-    from oracle import wtower_oracle as wo
+    from bench import host_cpus
+    from oracle import wtower_port as wp
+    cpus = host_cpus()
+    threads = wp.set_threads(cpus["usable"])
     uvw = uvw_dev.cpu().numpy().astype(np.float64)
-    vis = vis_dev.cpu().numpy().astype(np.complex128)
-    R, C = vis.shape
-    S = args.subgrid
-    eff = int(math.floor(S * 2.0 / 3.0))
-    eff_dist = eff / theta
-    ws_dist = H * w_step
-    s0 = np.zeros(R, np.int64)
-    e0 = np.full(R, C, np.int64)
-    sw, ew = wo.clamp_rows_vec(uvw[:, 2], C_0, C_0 / 200, s0, e0,
-                               -ws_dist / 2, ws_dist / 2)
-    plan = wo.WtowerPlan(args.image, S, theta, w_step, 0.0, 0.0,
-                         KW["support"], KW["oversampling"], KW["w_support"],
-                         KW["w_oversampling"])
-    n_vis, dt, done = 0, 0.0, 0
-    for iu, iv in [(0, 0), (1, 0), (0, 1), (-1, 0), (0, -1), (1, 1),
-                   (-1, -1), (2, 0)][:args.cpu_sample_subgrids]:
-        su, eu = wo._uv_clamp(uvw, C_0, C_0 / 200, sw, ew, iu, iv, eff_dist)
-        rows = np.nonzero(eu > su)[0]
-        if len(rows) == 0:
-            continue
-        sub = np.zeros((S, S), complex)
-        t0 = time.perf_counter()
-        plan.grid(vis[rows], uvw[rows], su[rows], eu[rows], C_0, C_0 / 200,
-                  sub, iu * eff, iv * eff, 0)
-        wo.fft_shift(sub, True)
-        dt += time.perf_counter() - t0
-        n_vis += int(np.sum(eu[rows] - su[rows]))
-        done += 1
-    return {"value": round(n_vis / dt / 1e6, 6) if dt else None,
-            "unit": "Mvis/s", "cores": 1, "kind": "port",
-            "sample": (f"oracle/wtower_oracle.py (numpy, 1 thread) sub-grid "
-                       f"towers of {done} sub-grids of the central w-stack "
-                       f"plane ({n_vis} vis, {dt:.1f} s); the per-plane "
-                       f"{args.image}^2 FFT and correction are excluded")}
+    vis = vis_dev.cpu().numpy()
+    plan = wp.Plan(vis, C_0, C_0 / 200, uvw, args.image, args.subgrid, theta,
+                   w_step, KW["support"], KW["oversampling"],
+                   KW["w_support"], KW["w_oversampling"], 0.0, H)
+    planes = plan.planes()
+    iw = planes[len(planes) // 2]
+    k = max(1, args.cpu_task_stride)
+    t0 = time.perf_counter()
+    n_s, done, present = plan.grid_towers(iw, k, 0)
+    t1 = time.perf_counter()
+    image = np.zeros((args.image, args.image), np.float32)
+    plan.finish_plane(iw, image)
+    t2 = time.perf_counter()
+    # all visibilities of the plane (the stride-1 clamp count, no gridding)
+    n_plane = int(np.sum(_plane_vis(uvw, args.chan, H * w_step, iw)))
+    t_proj = (t1 - t0) * present / max(done, 1) + (t2 - t1)
+    return {"value": round(n_plane / t_proj / 1e6, 6), "unit": "Mvis/s",
+            "cores": threads, "kind": "port", "host_cpus": cpus,
+            "sample": (f"oracle/wtower_port.c (C/OpenMP, {threads} threads) "
+                       f"w-stack plane {iw} of {len(planes)}: towers of "
+                       f"{done} of {present} non-empty sub-grid tasks "
+                       f"({n_s} vis, {t1 - t0:.1f} s), then the full "
+                       f"{args.image}^2 plane FFT + correction + "
+                       f"accumulation ({t2 - t1:.1f} s); projected plane "
+                       f"time {t_proj:.1f} s for {n_plane} vis"),
+            "towers_s": round(t1 - t0, 3), "plane_fft_correct_s":
+            round(t2 - t1, 3)}
+
+
+def _plane_vis(uvw, num_chan, ws_dist, iw):
+    """Visibilities of each row on w-stack plane iw (clamp_channels)."""
+    from oracle import wtower_oracle as wo
+    import numpy as np
+    R = uvw.shape[0]
+    s, e = wo.clamp_rows_vec(uvw[:, 2], C_0, C_0 / 200,
+                             np.zeros(R, np.int64),
+                             np.full(R, num_chan, np.int64),
+                             iw * ws_dist - ws_dist / 2,
+                             (iw + 1) * ws_dist - ws_dist / 2)
+    return e - s
 
 
 def roofline(tm, kernel):
@@ -239,7 +256,7 @@ def main():
         try:
             cpu = cpu_baseline(uvw, vis, args, theta, w_step, H)
         except Exception as exc:  # baseline failure must not hide the bench
-            cpu = {"value": None, "unit": "Mvis/s", "cores": 1,
+            cpu = {"value": None, "unit": "Mvis/s", "cores": None,
                    "kind": "port", "sample": f"failed: {exc!r}"}
 
     if rank == 0:
