@@ -110,3 +110,82 @@ def weighting_loops(uvw, freq_hz, max_abs_uv, grid, inp, out, robust=None):
                 out[t, b, c, p] = wt(1.0 / g)
             else:
                 out[t, b, c, p] = wt(float(inp[t, b, c, p]) / (1.0 + r * g))
+
+
+# -- tiled Briggs weighting (sdp_opt_weighting) ------------------------------
+
+def opt_briggs_runs(sorted_uu, sorted_vv, weights, sorted_tile, tile_offsets,
+                    grid_size, robust, out, index=None):
+    """sdp_optimized_weighting (index None: weights are the sorted weights,
+    out is indexed by entry) / sdp_optimised_indexed_weighting (index =
+    sorted_vis_index: weights and out indexed through it). Restates the
+    per-run algorithm of sdp_opt_weighting.cu:21-126 / :131-273 with the
+    reference's defects removed as include/ska-sdp-func/visibility/
+    sdp_opt_weighting.h lists them: run b = [tile_offsets[b],
+    tile_offsets[b + 1]) for b < num_tiles - 1, tile decoded from
+    sorted_tile[start], cell = round(pos) + grid_size / 2 - tile origin,
+    W = per-cell weight sums, R from sums over the run's in-tile entries.
+    One plain loop per run (test sizes)."""
+    tu, tv = 32, 16
+    centre = grid_size // 2
+    top_u = centre - (centre // tu) * tu - tu // 2
+    top_v = centre - (centre // tv) * tv - tv // 2
+    ntiles = ((grid_size + tu - 1) // tu) * ((grid_size + tv - 1) // tv)
+    numerator = (5.0 * 1 / (10.0 ** robust)) ** 2
+    wflat = weights.reshape(-1)
+    oflat = out.reshape(-1)
+    for b in range(ntiles - 1):
+        s, e = int(tile_offsets[b]), int(tile_offsets[b + 1])
+        if e <= s:
+            continue
+        code = int(sorted_tile[s])
+        tile_u = (code & 32767) * tu + top_u
+        tile_v = (code >> 15) * tv + top_v
+        cells = []
+        for i in range(s, e):
+            gu = int(_cround(sorted_uu[i])) + centre - tile_u
+            gv = int(_cround(sorted_vv[i])) + centre - tile_v
+            if 0 <= gu < tu and 0 <= gv < tv:
+                src = i if index is None else int(index[i])
+                cells.append((i, gu * tv + gv, src))
+        W = np.zeros(tu * tv)
+        for _, c, src in cells:
+            W[c] += wflat[src]
+        sw = sum(W[c] for _, c, _ in cells)
+        sw2 = sum(W[c] * W[c] for _, c, _ in cells)
+        if not cells:
+            continue
+        rob = numerator / (sw2 / sw)
+        for i, c, src in cells:
+            oflat[src] = wflat[src] / (1 + rob * W[c])
+    return out
+
+
+def _cround(x):
+    """C round(): half away from zero."""
+    return np.sign(x) * np.floor(np.abs(x) + 0.5)
+
+
+def briggs_global_test_reference(uvw, freqs, max_abs_uv, grid_size, robust,
+                                 inp):
+    """The reference test's own expected values for the indexed form
+    (tests/visibility/test_opt_weighting.py:20-106 of the reference:
+    reference_briggs_weights, a global Briggs weighting on a max_abs_uv
+    grid), restated vectorised."""
+    T, B, C, P = inp.shape
+    out = np.zeros_like(inp)
+    grid = np.zeros((grid_size, grid_size, P))
+    f = freqs / C_0
+    gu = uvw[:, :, 0:1] * f
+    gv = uvw[:, :, 1:2] * f
+    iu = (np.floor(gu / max_abs_uv * grid_size / 2) + grid_size / 2).astype(int)
+    iv = (np.floor(gv / max_abs_uv * grid_size / 2) + grid_size / 2).astype(int)
+    ok = (iu < grid_size) & (iv < grid_size)
+    for p in range(P):
+        np.add.at(grid[:, :, p], (iu[ok], iv[ok]), inp[..., p][ok])
+    g = grid[iu.clip(max=grid_size - 1), iv.clip(max=grid_size - 1)]  # T,B,C,P
+    sw = np.sum(np.where(ok[..., None], g, 0))
+    sw2 = np.sum(np.where(ok[..., None], g * g, 0))
+    rob = (5.0 * (1 / (10.0 ** robust))) ** 2 / (sw2 / sw)
+    out = np.where(ok[..., None], inp / (1 + rob * g), out)
+    return out
