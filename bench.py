@@ -531,6 +531,14 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
+                # Counter-based view of the same launch: PMC HBM bytes over
+                # the event time (the scatter skips empty tiles, so its
+                # algorithmic count includes grid bytes it never writes).
+                "traffic_GBs": (round(traffic / (avg[dom] * 1e-3) / 1e9, 1)
+                                if traffic and avg.get(dom) else None),
+                "traffic_frac": (round(traffic / (avg[dom] * 1e-3) / 1e9
+                                       / HBM_PEAK_GBS, 4)
+                                 if traffic and avg.get(dom) else None),
                 "algorithmic_bytes_per_launch": kern_bytes[dom],
             },
             "call_roofline": {

@@ -23,14 +23,19 @@ A restatement (float64 / complex128 throughout) of ska-sdp-func 1.2.2:
   sdp_grid_wstack_wtower.cpp    grid_all :467-700, degrid_all :218-448
 Used only by tests/ as the checker of the HIP implementation.
 
-Parity status: PARITY UNPINNED against reference outputs. The reference
-holds no golden vectors or fixtures for this path (its tests compare the
-C++ against an in-file NumPy model), and running or importing reference
-code here was refused ("Denied"). The restatement is instead
-cross-checked by identities the reference algorithm must satisfy: degridding
-reproduces the direct Fourier sum to the PSWF kernels' accuracy, gridding
-is the exact adjoint of degridding, and the PSWF values agree with
-scipy.special.pro_ang1 (the Zhang & Jin algorithm the reference ports).
+Parity status: pinned by the reference's own accuracy recipe, not by
+reference outputs. The reference holds no golden vectors for this path (its
+tests compare the C++ against an in-file NumPy model), and running or
+importing reference code was refused ("Denied"). The
+restatement is checked by identities the reference algorithm must satisfy
+(degridding reproduces the direct Fourier sum to the PSWF kernels'
+accuracy, gridding is the exact adjoint of degridding, the PSWF values
+agree with scipy.special.pro_ang1), and the HIP path it checks passes the
+reference C test's VLA recipe (test_gridder_wtower_uvw.cpp:264-330,
+:408-649: RMS vs direct Fourier sums < 1e-3; tests/test_wtower_vla_gpu.py)
+and its Python test's C++-vs-NumPy bound for degridded visibilities (atol
+1e-14 / rtol 1e-13, test_gridder_wtower_uvw.py:1642-1651;
+tests/test_wtower_gpu.py).
 """
 import math
 
