@@ -1,9 +1,11 @@
 """Throughput of the SURVEY §8(f) rows on one GPU, inputs resident in HBM:
-point-source DFT (dft_point_v01), uniform / Briggs weighting and
-degrid_uvw_custom, each with the numpy oracle timed beside it on a bounded
-slice of the same workload (single-threaded numpy, kind "port").
+point-source DFT (dft_point_v01), uniform / Briggs weighting, the tiled
+Briggs weighting (optimised_indexed_weighting after count_and_prefix_sum +
+tiled_indexing) and degrid_uvw_custom, each with the numpy oracle timed
+beside it on a bounded slice of the same workload (single-threaded numpy,
+kind "port").
 
-  python scripts/bench_next.py [--which dft weighting degrid]
+  python scripts/bench_next.py [--which dft weighting optw degrid]
 
 Prints one JSON line per function: rate, ms per call, the roofline
 quantity (FP64 phasor rate for the DFT, algorithmic HBM bytes for the
@@ -111,6 +113,84 @@ def bench_weighting(torch, dev, np, reps):
                              "kind": "port", "sample": "oracle briggs, 2 times"}}
 
 
+def bench_opt_weighting(torch, dev, np, reps):
+    import ctypes
+    from ska_sdp_func.visibility import (count_and_prefix_sum,
+                                         optimised_indexed_weighting,
+                                         tiled_indexing)
+    from oracle import weighting_oracle as wo
+    T, B, C, P, G, cell, sup = 64, 8192, 64, 1, 4096, 2.0e-5, 4
+    rng = np.random.default_rng(4)
+    freq = 100e6 + 1e5 * np.arange(C)
+    # positions (grid cells) = uvw f / c G cell: a disk reaching 0.45 G
+    r = 0.45 * G / (freq[-1] / 299792458.0 * G * cell) * np.sqrt(
+        rng.random((T, B)))
+    ph = 2 * np.pi * rng.random((T, B))
+    uvw = np.stack([r * np.cos(ph), r * np.sin(ph), np.zeros((T, B))], -1)
+    w_in = rng.random((T, B, C, P)) + 0.5
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_uvw, d_freq, d_w = d(uvw), d(freq), d(w_in)
+    d_vis = torch.zeros((T, B, C, P), dtype=torch.complex128, device=dev)
+    ntu, ntv = (G + 31) // 32, (G + 15) // 16
+    off = torch.zeros(ntu * ntv + 1, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(ntu * ntv, dtype=torch.int32, device=dev)
+    sk = torch.zeros(1, dtype=torch.int32, device=dev)
+    n = ctypes.c_int(0)
+    count_and_prefix_sum(d_uvw, d_freq, d_vis, G, 32, 16, cell, sup, n, off,
+                         cnt, sk)
+    N = n.value
+    tl = torch.zeros(N, dtype=torch.int32, device=dev)
+    vi = torch.zeros(N, dtype=torch.int32, device=dev)
+    uu = torch.zeros(N, dtype=torch.float64, device=dev)
+    vv = torch.zeros(N, dtype=torch.float64, device=dev)
+    off0 = off.clone()
+
+    def sort():
+        off.copy_(off0)
+        tiled_indexing(d_uvw, d_freq, G, 32, 16, cell, sup, C, B, T, tl, uu,
+                       vv, vi, off)
+    sort()
+    offs = off.clone()
+    out = torch.zeros_like(d_w)
+
+    def weigh():
+        optimised_indexed_weighting(d_uvw, d_vis, d_w, 0.5, G, cell, sup, n,
+                                    tl, uu, vv, vi, offs, cnt, out)
+    t_sort = timed(sort, torch.cuda.synchronize, reps)
+    t_w = timed(weigh, torch.cuda.synchronize, reps)
+    nv = T * B * C
+    # Per entry: positions 16 B + tile code 4 + index 4, read three times;
+    # per visibility one weight read twice (gather) and one written.
+    bytes_w = N * (16 + 4 + 4) * 3 + nv * P * 8 * 3
+    # CPU: the oracle's per-run loop over the first runs of the same arrays
+    h = {k: v.cpu().numpy() for k, v in dict(uu=uu, vv=vv, tl=tl,
+                                              vi=vi).items()}
+    ho = offs.cpu().numpy()
+    k = 0
+    while k + 1 < len(ho) and ho[k + 1] - ho[0] < 20000:
+        k += 1
+    sub = ho.copy()
+    sub[k + 1:] = ho[k]
+    t0 = time.perf_counter()
+    wo.opt_briggs_runs(h["uu"], h["vv"], w_in, h["tl"], sub, G, 0.5,
+                       np.zeros_like(w_in), index=h["vi"])
+    tc = time.perf_counter() - t0
+    return {"function": "sdp_optimised_indexed_weighting", "workload":
+            f"{T} times x {B} baselines x {C} channels, grid {G}^2, tiles "
+            f"32 x 16, support {sup}: {N} tile entries",
+            "ms_per_call_weighting": round(1e3 * t_w, 3),
+            "ms_per_call_tiled_indexing": round(1e3 * t_sort, 3),
+            "gvis_s_weighting": round(nv / t_w / 1e9, 2),
+            "roofline_weighting": {"bound": "hbm", "achieved_GBs":
+                                   round(bytes_w / t_w / 1e9, 1),
+                                   "frac": round(bytes_w / t_w / 1e9
+                                                 / HBM_PEAK, 3)},
+            "cpu_baseline": {"mentries_s": round(int(ho[k] - ho[0]) / tc
+                                                 / 1e6, 4),
+                             "cores": 1, "kind": "port",
+                             "sample": f"oracle per-run loop, {k} runs"}}
+
+
 def bench_degrid(torch, dev, np, reps):
     from ska_sdp_func.grid_data import degrid_uvw_custom
     from oracle import degrid_custom_oracle as dco
@@ -146,11 +226,13 @@ def main():
     import numpy as np
     import torch
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", nargs="+", default=["dft", "weighting", "degrid"])
+    ap.add_argument("--which", nargs="+",
+                    default=["dft", "weighting", "optw", "degrid"])
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     dev = torch.device("cuda:0")
-    fns = {"dft": bench_dft, "weighting": bench_weighting, "degrid": bench_degrid}
+    fns = {"dft": bench_dft, "weighting": bench_weighting,
+           "optw": bench_opt_weighting, "degrid": bench_degrid}
     for w in args.which:
         print(json.dumps(fns[w](torch, dev, np, args.reps)), flush=True)
 
