@@ -21,6 +21,21 @@
 #include "es_image_dev.h"
 #include "../utility/sdp_hip.h"
 
+// Waves per SIMD of the column passes (VGPR budget). Column pass A and
+// the degrid image pass fit 128 VGPRs without spills at 4 (3 at 131-132
+// VGPRs): config 2 gridding 7382 -> 7466 Mvis/s (FFT phase 0.310 -> 0.314
+// ms, image phase 0.171 -> 0.151 ms), degridding 6362 -> 6389 (A/B, three
+// alternating rounds on one box). Column pass B (149 VGPRs with the image
+// values it adds to held across the transform) spills at 4 (image phase
+// 0.32 ms); loading those values after the transform instead (103 VGPRs,
+// 4-5 waves) measured 0.164-0.175 ms.
+#ifndef SDP_COLA_WAVES
+#define SDP_COLA_WAVES 4
+#endif
+#ifndef SDP_COLB_WAVES
+#define SDP_COLB_WAVES 3
+#endif
+
 namespace sdp_es {
 namespace {
 
@@ -593,7 +608,7 @@ k_rows_grid(float2* __restrict__ grid, int k0, int M,
 // Column pass A (inverse): for u1 = blockIdx.x, length-N2 FFTs over rows
 // u1 + N1 * n2, times W^(u1 k2)*, back into rows u1 + N1 * k2.
 template<int N1, int N2, int SIGN = 1>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_COLA_WAVES)))
 k_cols_a_grid(float2* __restrict__ grid, int M, const float2* __restrict__ W)
 {
     constexpr int G = N1 * N2, B = ColPlan<N2>::B;
@@ -634,7 +649,7 @@ k_cols_a_grid(float2* __restrict__ grid, int M, const float2* __restrict__ W)
 // (conv_corr_and_scaling, sdp_gridder_uvw_es_fft.cpp:706-740); 3-D:
 // dirty += checker * Re(F * phasor(w)) (apply_w_screen_and_sum, :664-700).
 template<int N1, int N2, bool DO_W>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_COLB_WAVES)))
 k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
         ImageParams<float> ip, int plane, int k0, int M,
         const float2* __restrict__ W)
@@ -752,7 +767,7 @@ k_cols_b_block(float2* __restrict__ grid, int M, const float2* __restrict__ W)
 // sdp_gridder_uvw_es_fft.cpp:790-880): 2-D corrects the image in place and
 // applies the checker; 3-D applies checker * phasor(w).
 template<int N1, int N2, bool DO_W>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_COLA_WAVES)))
 k_cols_a_image(float* __restrict__ dirty, int correct_in_place,
         float2* __restrict__ grid, ImageParams<float> ip, int plane, int k0,
         int M, const float2* __restrict__ W)
