@@ -290,6 +290,66 @@ def run_config3(args, torch, dev, dist, world, rank):
     return out
 
 
+def cpu_baseline_wtower(args, uvw_dev, freq_dev, vis_dev, px):
+    """the reference's own CPU imaging gridder on the same
+    visibilities -- the C/OpenMP port of sdp_grid_wstack_wtower_grid_all
+    (oracle/wtower_port.c, checked against the numpy restatement) on the
+    job's host-CPU share, image 8192^2 at the config's pixel size (theta =
+    8192 px; the reference has no CPU ES gridder). Every w-stack plane's
+    towers are run for every 8th non-empty sub-grid task (hashed) and
+    projected to all tasks; the plane FFT + correction is run once and
+    counted once per plane."""
+    import numpy as np
+    import ska_sdp_func.grid_data as g
+    from oracle import wtower_port as wp
+    cpus = host_cpus()
+    threads = wp.set_threads(cpus["usable"])
+    N, S, k = 8192, 256, 8
+    theta = N * px
+    fov = 0.8 * theta
+    w_step = g.determine_w_step(theta, fov, 0.0, 0.0)
+    H = float(g.determine_max_w_tower_height(
+        S, theta, fov, w_step, 8, 16384, 8, 16384, image_size=2 * S,
+        subgrid_frac=2.0 / 3.0))
+    uvw = uvw_dev.cpu().numpy().astype(np.float64)
+    vis = vis_dev.cpu().numpy()
+    f = freq_dev.cpu().numpy().astype(np.float64)
+    df = float(f[1] - f[0]) if len(f) > 1 else 0.0
+    plan = wp.Plan(vis, float(f[0]), df, uvw, N, S, theta, w_step, 8, 16384,
+                   8, 16384, 0.0, H)
+    t_towers, n_planes, n_vis, done_t, present_t = 0.0, 0, 0, 0, 0
+    busiest = None
+    for iw in plan.planes():
+        t0 = time.perf_counter()
+        n_s, done, present = plan.grid_towers(iw, k, 0)
+        dt = time.perf_counter() - t0
+        if present == 0:
+            continue
+        n_planes += 1
+        t_towers += dt * present / max(done, 1)
+        done_t += done
+        present_t += present
+        if busiest is None or present > busiest[1]:
+            busiest = (iw, present)
+    image = np.zeros((N, N), np.float32)
+    t0 = time.perf_counter()
+    plan.finish_plane(busiest[0], image)
+    t_plane = time.perf_counter() - t0
+    total = args.rows * args.chan
+    t_proj = t_towers + n_planes * t_plane
+    return {"value": round(total / t_proj / 1e6, 4), "unit": "Mvis/s",
+            "cores": threads, "kind": "port",
+            "sample": (f"oracle/wtower_port.c (C/OpenMP port of the "
+                       f"reference grid_all, {threads} threads) on the "
+                       f"config's {total} visibilities, image {N}^2, "
+                       f"theta {theta:.4f}, sub-grid {S}, W = W_w = 8, "
+                       f"w_step {w_step:.1f}, tower height {H:g}: towers of "
+                       f"{done_t} of {present_t} sub-grid tasks over "
+                       f"{n_planes} w-stack plane(s), projected "
+                       f"{t_towers:.1f} s, + plane FFT/correction "
+                       f"{t_plane:.2f} s x {n_planes}")}
+
+
 def main():
     args = parse()
     import torch
@@ -488,12 +548,18 @@ def main():
         config3 = run_config3(args, torch, dev, dist, world, rank)
 
     cpu = None
+    cpu_wt = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(args, G, W, plan.beta, G * px)
         except Exception as exc:  # baseline failure must not hide the bench
             cpu = {"value": None, "unit": "Mvis/s", "cores": 0,
                    "kind": "port", "sample": f"failed: {exc!r}"}
+        try:
+            cpu_wt = cpu_baseline_wtower(args, uvw, freq, vis, px)
+        except Exception as exc:
+            cpu_wt = {"value": None, "unit": "Mvis/s", "cores": 0,
+                      "kind": "port", "sample": f"failed: {exc!r}"}
 
     if rank == 0:
         line = {
@@ -559,6 +625,9 @@ def main():
                                                     * 1e-3) / 1e6, 3)
                                  if degrid else None),
             "cpu_baseline": cpu,
+            # the reference's CPU imaging gridder (w-towers)
+            # on the same visibilities, beside the like-for-like ES port.
+            "cpu_baseline_reference_gridder": cpu_wt,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
