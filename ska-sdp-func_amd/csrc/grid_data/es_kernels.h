@@ -4,7 +4,8 @@
 //   bucket_count -> scan_columns -> scan_bins -> bucket_fill -> (grid) zero_hot_tiles + scatter_tiles
 //                     (degrid) gather_tiles
 // Visibilities are bucketed by 64x64 grid tile (counting sort, LDS-private
-// histograms per chunk of visibilities). In grid mode a visibility is listed
+// histograms per chunk of visibilities; records move in two levels: by
+// super bin of S x S tiles with LDS-staged coalesced stores, then by tile). In grid mode a visibility is listed
 // in every tile its support touches and each tile only accumulates the taps
 // that fall inside it, so every grid cell has exactly one owning workgroup:
 // the tile is accumulated in LDS (ds_add) and written to HBM ONCE with plain
@@ -27,6 +28,8 @@ constexpr int kCoarseTile = kTile * kCoarse;   // 256 cells
 constexpr int kBinsPerPass = 16384;    // LDS histogram capacity (64 KiB)
 constexpr int kPiece = 4096;           // max entries per scatter work item
 constexpr int kMaxChunks = 1024;       // chunks of visibilities per bucketing
+constexpr int kMaxSuperBins = 1024;    // super bins (first bucketing level)
+constexpr int kMaxSuperTiles = 4096;   // tiles per super bin (S^2, S <= 64)
 constexpr int kTapPolyPairs = 3;       // interior taps 1..6 of W = 8
 constexpr int kTapPolyDeg = 10;        // ~1e-9 relative (f32 Horner ~5e-7)
 
@@ -46,6 +49,10 @@ struct EsParams
     int nbins;          // tile bins, block-major: 16 per 4 x 4-tile block
                         // (bin b: block b / 16, tile (b % 16) / 4, b % 4),
                         // so consecutive work items touch adjacent tiles
+    int sshift;         // super bins (first bucketing level): S x S tiles,
+    int nsuper;         // S = 1 << sshift >= 8, nsuper = ceil(ntiles / S)
+    int nsbins;         // per axis, nsbins = nsuper^2 <= kMaxSuperBins
+    int tstride;        // count table row: nbins tile counts | nsbins super
     T beta;             // full beta (table value * W)
     T uv_scale;         // G * pixel_size
     T w_scale;
@@ -66,22 +73,29 @@ void es_tap_poly_fit(double beta_f32, float out[kTapPolyPairs]
 // Scratch owned by a plan (device pointers).
 struct BucketScratch
 {
-    uint32_t* table = nullptr;      // [num_chunks][nbins] counts / offsets
-    uint32_t* bin_count = nullptr;  // [nbins]
+    uint32_t* table = nullptr;      // [num_chunks][tstride] counts / offsets
+    uint32_t* bin_count = nullptr;  // [tstride]: tile then super-bin totals
     uint32_t* bin_start = nullptr;  // [nbins + 1]
     uint32_t* item_start = nullptr; // [nbins + 1]
     uint32_t* totals = nullptr;     // [2]: entries, items
+    uint32_t* sb_start = nullptr;   // [nsbins + 1]: super-bin starts
     uint32_t* item_bin = nullptr;   // [item_capacity]: work item -> bin
     uint32_t item_capacity = 0;
     void* recs = nullptr;           // bucketed records (worst-case size)
+    void* recs1 = nullptr;          // first level, by super bin (same size)
     size_t recs_bytes = 0;
     size_t table_entries = 0;
 };
 
-// Number of visibility chunks used for a given visibility count and bin
-// count (the chunk-by-bin count table stays below 2^31 bytes, the range of
-// the buffer addressing in k_scan_columns).
-int num_chunks(int64_t num_vis, int nbins);
+// Number of visibility chunks used for a given visibility count and count
+// table row length (the chunk-by-bin table stays below 2^31 bytes, the
+// range of the buffer addressing in k_scan_columns).
+int num_chunks(int64_t num_vis, int tstride);
+
+// Super-bin geometry for ntiles tiles per axis: sets sshift, nsuper, nsbins
+// (the smallest S = 2^sshift >= 8 with ceil(ntiles / S)^2 <= kMaxSuperBins).
+// Returns false if none exists within kMaxSuperTiles.
+bool super_geometry(int ntiles, int* sshift, int* nsuper, int* nsbins);
 
 // Bucketing, fully asynchronous: fills scratch.recs (sized by the caller
 // for the worst case, 4 entries per visibility) and the work-item table;

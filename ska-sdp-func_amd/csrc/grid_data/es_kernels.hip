@@ -228,21 +228,38 @@ __device__ __forceinline__ int fine_bin(const EsParams<T>& p, int tu, int tv)
 
 // Bucketing kernels ---------------------------------------------------------
 
+// Tile range of a footprint (grid mode: every tile the support touches;
+// degrid: the tile of the first tap) and its super-bin range.
+template<typename T, int MODE>
+__device__ __forceinline__ void tile_span(const EsParams<T>& p, int u0, int u1,
+        int v0, int v1, int& tu0, int& tu1, int& tv0, int& tv1)
+{
+    const int half = p.G / 2;
+    tu0 = (u0 + half) / kTile;
+    tv0 = (v0 + half) / kTile;
+    tu1 = MODE == MODE_GRID ? (u1 + half) / kTile : tu0;
+    tv1 = MODE == MODE_GRID ? (v1 + half) / kTile : tv0;
+}
+
 template<typename T, int MODE, int NT>
 __global__ __launch_bounds__(NT) void k_bucket_count(EsParams<T> p,
         int64_t num_rows, int num_chan, int64_t chunk, const T* __restrict__ uvw,
         const T* __restrict__ freq, uint32_t* __restrict__ table)
 {
     __shared__ uint32_t hist[kBinsPerPass];
+    __shared__ uint32_t shist[kMaxSuperBins];
     const int pass_base = blockIdx.y * kBinsPerPass;
     const int nb = min(kBinsPerPass, p.nbins - pass_base);
+    // Pass 0 also counts records per super bin (one per visibility and
+    // super bin its tiles touch: the first level of k_bucket_fill1).
+    const bool supers = blockIdx.y == 0;
     for (int i = threadIdx.x; i < nb; i += NT) hist[i] = 0;
+    for (int i = threadIdx.x; i < p.nsbins; i += NT) shist[i] = 0;
     __syncthreads();
     // Chunks are ranges of rows; a thread takes a row and its channels
     // (no 64-bit division per visibility, uvw read once per row).
     const int64_t r0 = (int64_t)blockIdx.x * chunk;
     const int64_t r1 = min(num_rows, r0 + chunk);
-    const int half = p.G / 2;
     for (int64_t r = r0 + threadIdx.x; r < r1; r += NT)
     {
         const T u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2];
@@ -250,28 +267,26 @@ __global__ __launch_bounds__(NT) void k_bucket_count(EsParams<T> p,
         {
             Footprint<T> f;
             if (!footprint(p, u, v, w, freq[c], f)) continue;
-            if (MODE == MODE_GRID)
-            {
-                const int tu0 = (f.u0 + half) / kTile, tu1 = (f.u1 + half) / kTile;
-                const int tv0 = (f.v0 + half) / kTile, tv1 = (f.v1 + half) / kTile;
-                for (int tu = tu0; tu <= tu1; ++tu)
-                    for (int tv = tv0; tv <= tv1; ++tv)
-                    {
-                        const int b = fine_bin(p, tu, tv) - pass_base;
-                        if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
-                    }
-            }
-            else
-            {
-                const int b = fine_bin(p, (f.u0 + half) / kTile,
-                        (f.v0 + half) / kTile) - pass_base;
-                if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
-            }
+            int tu0, tu1, tv0, tv1;
+            tile_span<T, MODE>(p, f.u0, f.u1, f.v0, f.v1, tu0, tu1, tv0, tv1);
+            for (int tu = tu0; tu <= tu1; ++tu)
+                for (int tv = tv0; tv <= tv1; ++tv)
+                {
+                    const int b = fine_bin(p, tu, tv) - pass_base;
+                    if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
+                }
+            if (supers)
+                for (int su = tu0 >> p.sshift; su <= tu1 >> p.sshift; ++su)
+                    for (int sv = tv0 >> p.sshift; sv <= tv1 >> p.sshift; ++sv)
+                        atomicAdd(&shist[su * p.nsuper + sv], 1u);
         }
     }
     __syncthreads();
-    uint32_t* row = table + (size_t)blockIdx.x * p.nbins + pass_base;
-    for (int i = threadIdx.x; i < nb; i += NT) row[i] = hist[i];
+    uint32_t* row = table + (size_t)blockIdx.x * p.tstride;
+    for (int i = threadIdx.x; i < nb; i += NT) row[pass_base + i] = hist[i];
+    if (supers)
+        for (int i = threadIdx.x; i < p.nsbins; i += NT)
+            row[p.nbins + i] = shist[i];
 }
 
 // Per bin: exclusive prefix over chunks (in place) and the bin total.
@@ -279,6 +294,7 @@ __global__ __launch_bounds__(NT) void k_bucket_count(EsParams<T> p,
 __global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
         int num_chunks, int nbins, uint32_t* __restrict__ bin_count)
 {
+    // nbins = columns = the table row length (tile and super-bin counts).
     __shared__ uint32_t part[16][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = blockIdx.x * 64 + lane;
@@ -502,78 +518,341 @@ __device__ __forceinline__ void store_rec(T* dst, const T (&rec)[W])
     }
 }
 
+// Barrier for LDS hand-offs only: unlike __syncthreads it does not wait
+// for the wave's outstanding global loads and stores (s_waitcnt vmcnt(0)),
+// so prefetched loads and the record stores stay in flight across it.
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Exclusive scan of n <= kMaxSuperBins counts (LDS) into off (LDS); returns
+// the total. Callers synchronise before reading off or reusing s_wave.
+template<int NT>
+__device__ __forceinline__ uint32_t block_scan_counts(const uint32_t* cnt,
+        uint32_t* off, int n, uint32_t* s_wave)
+{
+    constexpr int E = (kMaxSuperBins + NT - 1) / NT;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t v[E];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+    {
+        const int i = t * E + e;
+        v[e] = i < n ? cnt[i] : 0u;
+        sum += v[e];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1)
+    {
+        const uint32_t x = __shfl_up(inc, o);
+        if (lane >= o) inc += x;
+    }
+    if (lane == 63) s_wave[wave] = inc;
+    lds_barrier();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w)
+    {
+        const uint32_t x = s_wave[w];
+        before += w < wave ? x : 0u;
+        total += x;
+    }
+    uint32_t run = before + inc - sum;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+    {
+        const int i = t * E + e;
+        if (i < n) off[i] = run;
+        run += v[e];
+    }
+    return total;
+}
+
+// 16-byte vector copy of one record.
+template<typename T, int W>
+__device__ __forceinline__ void copy_rec(T* dst, const T* src)
+{
+    constexpr int kPer = 16 / sizeof(T);
+    using V = __attribute__((ext_vector_type(kPer))) T;
+#pragma unroll
+    for (int k = 0; k < W; k += kPer) *(V*)(dst + k) = *(const V*)(src + k);
+}
+
+// Visibilities per thread per batch of the first level: 3 records of 16
+// bytes (1 of 32 or 64) per thread, so that the LDS stage of a 1024-thread
+// block stays below 80 KiB and two blocks share a CU (one block's loads
+// overlap the other's sort and stores).
+#ifndef SDP_FILL1_BYTES
+#define SDP_FILL1_BYTES 48
+#endif
+#ifndef SDP_FILL1_WAVES
+#define SDP_FILL1_WAVES 1   // blocks per CU (VGPR budget 128 / this)
+#endif
+#ifndef SDP_FILL2_GROUPS
+#define SDP_FILL2_GROUPS 64
+#endif
+template<typename T, int W>
+struct Fill1Shape
+{
+    static constexpr int K = (SDP_FILL1_BYTES / (W * (int)sizeof(T))) > 0 ?
+            SDP_FILL1_BYTES / (W * (int)sizeof(T)) : 1;
+};
+
+// First bucketing level: the chunk's records by super bin. A block walks
+// its chunk in batches of NT * K visibilities; each batch is counting-
+// sorted by super bin in LDS (ranks from LDS atomics, an exclusive scan of
+// the batch counts) and then stored in LDS order, so the records of one
+// super bin leave as one contiguous run of ~NT * K / nsbins records (full
+// cache lines) instead of one 16-byte store per record into a random bin.
+// Record layouts as k_bucket_fill's were: see es_kernels.h. Positions in
+// a super bin follow the chunk order (scanned count-table columns), which
+// lets k_bucket_fill2 find the records of any chunk range.
 template<typename T, int MODE, bool DO_W, int NT>
-__global__ __launch_bounds__(NT) void k_bucket_fill(EsParams<T> p,
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(
+        SDP_FILL1_WAVES * NT / 256))) void k_bucket_fill1(EsParams<T> p,
         int64_t num_rows, int num_chan, int64_t chunk, const T* __restrict__ uvw,
         const T* __restrict__ freq, const T* __restrict__ vis,
         const T* __restrict__ weight, const uint32_t* __restrict__ table,
-        const uint32_t* __restrict__ bin_start, T* __restrict__ recs)
+        const uint32_t* __restrict__ bin_count, uint32_t* __restrict__ sb_start,
+        T* __restrict__ recs1)
 {
-    __shared__ uint32_t cursor[kBinsPerPass];
     constexpr int kWords = Rec<T, MODE, DO_W>::kWords;
-    const int pass_base = blockIdx.y * kBinsPerPass;
-    const int nb = min(kBinsPerPass, p.nbins - pass_base);
-    const uint32_t* row = table + (size_t)blockIdx.x * p.nbins + pass_base;
-    for (int i = threadIdx.x; i < nb; i += NT)
-        cursor[i] = bin_start[pass_base + i] + row[i];
+    constexpr int K = Fill1Shape<T, kWords>::K;
+    constexpr int kBatch = NT * K;
+    constexpr int kCap = kBatch + kBatch / 8;   // staged records per round
+    __shared__ uint32_t cursor[kMaxSuperBins];
+    __shared__ uint32_t lcnt[kMaxSuperBins];
+    __shared__ uint32_t loff[kMaxSuperBins];
+    __shared__ uint32_t s_wave[NT / 64];
+    __shared__ __attribute__((aligned(16))) T stage[kCap * kWords];
+    __shared__ uint16_t stage_sb[kCap];
+    const int t = threadIdx.x;
+    const int nsb = p.nsbins;
+    // Super-bin starts (scan of the totals; block 0 stores them for
+    // k_bucket_fill2) + this chunk's offset in each.
+    const uint32_t n_sb = block_scan_counts<NT>(bin_count + p.nbins, loff,
+            nsb, s_wave);
+    __syncthreads();
+    const uint32_t* row = table + (size_t)blockIdx.x * p.tstride + p.nbins;
+    for (int i = t; i < nsb; i += NT)
+    {
+        cursor[i] = loff[i] + row[i];
+        lcnt[i] = 0;
+        if (blockIdx.x == 0) sb_start[i] = loff[i];
+    }
+    if (blockIdx.x == 0 && t == 0) sb_start[nsb] = n_sb;
     __syncthreads();
     const int64_t r0 = (int64_t)blockIdx.x * chunk;
     const int64_t r1 = min(num_rows, r0 + chunk);
-    const int half = p.G / 2;
-    // Threads walk the chunk's visibilities in memory order (consecutive
-    // lanes = consecutive channels of a row), so the vis / weight loads of
-    // a wave are coalesced for any channel count; the row's uvw is an L1
-    // hit shared by its channels.
-    // Trailing chunks can be empty (r0 >= num_rows when the rows do not
-    // fill all num_chunks chunks of ceil(rows / chunks) rows).
     const uint32_t nvis = r1 > r0 ? (uint32_t)((r1 - r0) * num_chan) : 0u;
-    for (uint32_t li = threadIdx.x; li < nvis; li += NT)
-    {
-        const uint32_t rl = num_chan == 1 ? li : li / (uint32_t)num_chan;
-        const int c = (int)(li - rl * (uint32_t)num_chan);
-        const int64_t r = r0 + rl;
-        const int64_t i = r * num_chan + c;
+    // The chunk's inputs from scalar base pointers (32-bit offsets); row of
+    // a visibility by a multiply-high with a one-step correction.
+    const T* __restrict__ uvw_c = uvw + 3 * r0;
+    const T* __restrict__ vis_c = MODE == MODE_GRID ? vis + 2 * r0 * num_chan : vis;
+    const T* __restrict__ wt_c = MODE == MODE_GRID ? weight + r0 * num_chan : weight;
+    const uint32_t nch = (uint32_t)num_chan;
+    const uint32_t magic = nch > 1 ? (uint32_t)(0x100000000ull / nch) : 0u;
+    // The inputs of a batch are loaded one batch ahead (K visibilities per
+    // thread; consecutive lanes = consecutive visibilities, so the vis /
+    // weight loads are coalesced and a row's uvw is shared by its
+    // channels): their latency overlaps the sort and stores of the batch
+    // before (the barriers below are LDS-only).
+    T in_u[K], in_v[K], in_w[K], in_f[K], in_re[K], in_im[K], in_wt[K];
+    auto load_batch = [&](uint32_t b0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
         {
-            const T u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2];
+            const uint32_t li = min(b0 + (uint32_t)(k * NT + t), nvis - 1);
+            uint32_t rl = li;
+            if (nch > 1)
+            {
+                rl = __umulhi(li, magic);
+                if (li - rl * nch >= nch) ++rl;
+            }
+            const uint32_t c = li - rl * nch;
+            in_u[k] = uvw_c[3 * rl];
+            in_v[k] = uvw_c[3 * rl + 1];
+            in_w[k] = uvw_c[3 * rl + 2];
+            in_f[k] = freq[c];
+            if constexpr (MODE == MODE_GRID)
+            {
+                in_re[k] = vis_c[2 * li];
+                in_im[k] = vis_c[2 * li + 1];
+                in_wt[k] = wt_c[li];
+            }
+        }
+    };
+    if (nvis) load_batch(0);
+    for (uint32_t base = 0; base < nvis; base += kBatch)
+    {
+        T rec[K][kWords];
+        uint32_t rank[K][2];
+        // Super bins of entry k: first sbase, + 1 (v) if bit 16, + nsuper
+        // (u) if bit 17; bit 18 = entry present.
+        uint32_t span[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+        {
+            span[k] = 0;
+            rank[k][0] = rank[k][1] = 0;
+            const uint32_t li = base + (uint32_t)(k * NT + t);
+            if (li >= nvis) continue;
             Footprint<T> f;
-            if (!footprint(p, u, v, w, freq[c], f)) continue;
-            T rec[kWords];
-            rec[0] = f.pu;
-            rec[1] = f.pv;
+            if (!footprint(p, in_u[k], in_v[k], in_w[k], in_f[k], f)) continue;
+            rec[k][0] = f.pu;
+            rec[k][1] = f.pv;
             if constexpr (MODE == MODE_GRID)
             {
                 // kernels.cu:163-167: weight, then conjugate for w < 0.
-                const T wt = weight[i];
-                rec[2] = vis[2 * i] * wt;
-                T vim = vis[2 * i + 1] * wt;
+                const T wt = in_wt[k];
+                rec[k][2] = in_re[k] * wt;
+                T vim = in_im[k] * wt;
                 vim *= f.flip;
-                rec[3] = vim;
+                rec[k][3] = vim;
                 if constexpr (DO_W && kWords == 8)
                 {
-                    rec[4] = f.kw;
-                    rec[5] = rec[6] = rec[7] = T(0);
+                    rec[k][4] = f.kw;
+                    rec[k][5] = rec[k][6] = rec[k][7] = T(0);
                 }
-                const int tu0 = (f.u0 + half) / kTile, tu1 = (f.u1 + half) / kTile;
-                const int tv0 = (f.v0 + half) / kTile, tv1 = (f.v1 + half) / kTile;
-                for (int tu = tu0; tu <= tu1; ++tu)
-                    for (int tv = tv0; tv <= tv1; ++tv)
-                    {
-                        const int b = fine_bin(p, tu, tv) - pass_base;
-                        if (b < 0 || b >= nb) continue;
-                        const uint32_t pos = atomicAdd(&cursor[b], 1u);
-                        store_rec<T, kWords>(recs + (size_t)pos * kWords, rec);
-                    }
             }
             else
             {
-                rec[2] = copysign(f.kw, f.flip);
-                rec[3] = idx_bits(T(0), (uint64_t)i);
-                const int b = fine_bin(p, (f.u0 + half) / kTile,
-                        (f.v0 + half) / kTile) - pass_base;
-                if (b < 0 || b >= nb) continue;
-                const uint32_t pos = atomicAdd(&cursor[b], 1u);
-                store_rec<T, kWords>(recs + (size_t)pos * kWords, rec);
+                rec[k][2] = copysign(f.kw, f.flip);
+                rec[k][3] = idx_bits(T(0),
+                        (uint64_t)(r0 * num_chan) + (uint64_t)li);
             }
+            int tu0, tu1, tv0, tv1;
+            tile_span<T, MODE>(p, f.u0, f.u1, f.v0, f.v1, tu0, tu1, tv0, tv1);
+            const int su0 = tu0 >> p.sshift, sv0 = tv0 >> p.sshift;
+            // A support (<= 64 cells) spans at most 2 super bins per axis.
+            span[k] = (uint32_t)(su0 * p.nsuper + sv0) | (1u << 18) |
+                    ((uint32_t)((tv1 >> p.sshift) - sv0) << 16) |
+                    ((uint32_t)((tu1 >> p.sshift) - su0) << 17);
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                {
+                    if ((a && !(span[k] & (1u << 17))) ||
+                            (b && !(span[k] & (1u << 16)))) continue;
+                    const int sb = (int)(span[k] & 0xFFFFu) + a * p.nsuper + b;
+                    const uint32_t q = atomicAdd(&lcnt[sb], 1u);
+                    rank[k][a] |= q << (16 * b);
+                }
+        }
+        if (base + kBatch < nvis) load_batch(base + kBatch);
+        lds_barrier();
+        const uint32_t total = block_scan_counts<NT>(lcnt, loff, nsb, s_wave);
+        lds_barrier();
+        // Rounds of kCap staged records (one round unless many visibilities
+        // of the batch straddle super bins).
+        for (uint32_t s0 = 0; s0 < total; s0 += kCap)
+        {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                    {
+                        if (!(span[k] & (1u << 18)) ||
+                                (a && !(span[k] & (1u << 17))) ||
+                                (b && !(span[k] & (1u << 16)))) continue;
+                        const int sb = (int)(span[k] & 0xFFFFu) + a * p.nsuper + b;
+                        const uint32_t slot = loff[sb] +
+                                ((rank[k][a] >> (16 * b)) & 0xFFFFu) - s0;
+                        if (slot >= (uint32_t)kCap) continue;
+                        store_rec<T, kWords>(stage + slot * kWords, rec[k]);
+                        stage_sb[slot] = (uint16_t)sb;
+                    }
+            lds_barrier();
+            const uint32_t n = min((uint32_t)kCap, total - s0);
+            for (uint32_t j = t; j < n; j += NT)
+            {
+                const int sb = stage_sb[j];
+                const uint32_t pos = cursor[sb] + (s0 + j - loff[sb]);
+                copy_rec<T, kWords>(recs1 + (size_t)pos * kWords,
+                        stage + j * kWords);
+            }
+            lds_barrier();
+        }
+        for (int i = t; i < nsb; i += NT)
+        {
+            cursor[i] += lcnt[i];
+            lcnt[i] = 0;
+        }
+        lds_barrier();
+    }
+}
+
+// Second level: the records of super bin blockIdx.y that come from chunks
+// [c0, c0 + gc) (contiguous in recs1) into their tiles. A record is
+// written to every tile of this super bin its support touches (grid) or
+// the tile of its first tap (degrid); tile f's records from these chunks
+// occupy [bin_start[f] + table[c0][f], ...), a window of a few hundred
+// bytes per tile that the block fills while it stays in L2.
+template<typename T, int MODE, bool DO_W>
+__global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
+        int gc, const uint32_t* __restrict__ table,
+        const uint32_t* __restrict__ bin_count,
+        const uint32_t* __restrict__ bin_start,
+        const uint32_t* __restrict__ sb_start, const T* __restrict__ recs1,
+        T* __restrict__ recs)
+{
+    constexpr int kWords = Rec<T, MODE, DO_W>::kWords;
+    __shared__ uint32_t cur[kMaxSuperTiles];
+    const int t = threadIdx.x, sb = blockIdx.y;
+    const int c0 = blockIdx.x * gc;
+    if (c0 >= nc) return;
+    const int c1 = min(nc, c0 + gc);
+    const int S = 1 << p.sshift;
+    const int su = sb / p.nsuper, sv = sb - su * p.nsuper;
+    const int tu_base = su << p.sshift, tv_base = sv << p.sshift;
+    for (int j = t; j < S * S; j += 256)
+    {
+        const int tu = tu_base + (j >> p.sshift), tv = tv_base + (j & (S - 1));
+        if (tu < p.ntiles && tv < p.ntiles)
+        {
+            const int f = fine_bin(p, tu, tv);
+            cur[j] = bin_start[f] + table[(size_t)c0 * p.tstride + f];
+        }
+    }
+    __syncthreads();
+    const uint32_t* col = table + p.nbins + sb;
+    const uint32_t e0 = sb_start[sb] + col[(size_t)c0 * p.tstride];
+    const uint32_t e1 = c1 < nc ? sb_start[sb] + col[(size_t)c1 * p.tstride] :
+            sb_start[sb + 1];
+    // Four records per thread in flight (loads issued before the LDS
+    // atomics and stores of the first).
+    constexpr int kIn = 4;
+    for (uint32_t e = e0 + t; e < e1; e += 256 * kIn)
+    {
+        T rec[kIn][kWords];
+#pragma unroll
+        for (int q = 0; q < kIn; ++q)
+            if (e + q * 256 < e1)
+                copy_rec<T, kWords>(rec[q], recs1 + (size_t)(e + q * 256) * kWords);
+#pragma unroll
+        for (int q = 0; q < kIn; ++q)
+        {
+            if (e + q * 256 >= e1) break;
+            int u0, u1, v0, v1, tu0, tu1, tv0, tv1;
+            tap_range(p, rec[q][0], rec[q][1], u0, u1, v0, v1);
+            tile_span<T, MODE>(p, u0, u1, v0, v1, tu0, tu1, tv0, tv1);
+            tu0 = max(tu0, tu_base); tu1 = min(tu1, tu_base + S - 1);
+            tv0 = max(tv0, tv_base); tv1 = min(tv1, tv_base + S - 1);
+            for (int tu = tu0; tu <= tu1; ++tu)
+                for (int tv = tv0; tv <= tv1; ++tv)
+                {
+                    const int j = ((tu - tu_base) << p.sshift) | (tv - tv_base);
+                    const uint32_t pos = atomicAdd(&cur[j], 1u);
+                    store_rec<T, kWords>(recs + (size_t)pos * kWords, rec[q]);
+                }
         }
     }
 }
@@ -1747,14 +2026,30 @@ int bucket_threads()
     return v;
 }
 
-int num_chunks(int64_t num_vis, int nbins)
+int num_chunks(int64_t num_vis, int tstride)
 {
     const int64_t cv = chunk_vis();
     const int64_t by_size = (num_vis + cv - 1) / cv;
     const int64_t by_table = (((int64_t)1 << 31) - 1) /
-            (4 * (int64_t)std::max(1, nbins));
+            (4 * (int64_t)std::max(1, tstride));
     return (int)std::max<int64_t>(1, std::min<int64_t>(
             std::min<int64_t>(kMaxChunks, by_table), by_size));
+}
+
+bool super_geometry(int ntiles, int* sshift, int* nsuper, int* nsbins)
+{
+    for (int sh = 3; (1 << (2 * sh)) <= kMaxSuperTiles; ++sh)
+    {
+        const int n = (ntiles + (1 << sh) - 1) >> sh;
+        if (n * n <= kMaxSuperBins)
+        {
+            *sshift = sh;
+            *nsuper = n;
+            *nsbins = n * n;
+            return true;
+        }
+    }
+    return false;
 }
 
 template<typename T, int MODE, int NT>
@@ -1766,14 +2061,24 @@ void launch_count(const dim3& g, const EsParams<T>& p, int64_t num_rows,
             chunk, uvw, freq, table);
 }
 
+// Both record levels: k_bucket_fill1 (chunk blocks) then k_bucket_fill2
+// (super bin x chunk-group blocks).
 template<typename T, int MODE, bool DO_W, int NT>
-void launch_fill(const dim3& g, const EsParams<T>& p, int64_t num_rows,
-        int num_chan, int64_t chunk, const T* uvw, const T* freq, const T* vis,
-        const T* weight, const uint32_t* table, const uint32_t* bin_start,
-        T* recs, hipStream_t stream)
+void launch_fill(int nc, int64_t chunk, const EsParams<T>& p,
+        int64_t num_rows, int num_chan, const T* uvw, const T* freq,
+        const T* vis, const T* weight, const BucketScratch* s,
+        hipStream_t stream)
 {
-    k_bucket_fill<T, MODE, DO_W, NT><<<g, NT, 0, stream>>>(p, num_rows,
-            num_chan, chunk, uvw, freq, vis, weight, table, bin_start, recs);
+    k_bucket_fill1<T, MODE, DO_W, NT><<<nc, NT, 0, stream>>>(p, num_rows,
+            num_chan, chunk, uvw, freq, vis, weight, s->table, s->bin_count,
+            s->sb_start, (T*)s->recs1);
+    // SDP_FILL2_GROUPS chunk groups: groups x nsbins blocks, each moving
+    // the records of nc / groups chunks of one super bin.
+    const int groups = std::min(nc, SDP_FILL2_GROUPS);
+    const int gc = (nc + groups - 1) / groups;
+    k_bucket_fill2<T, MODE, DO_W><<<dim3((nc + gc - 1) / gc, p.nsbins), 256,
+            0, stream>>>(p, nc, gc, s->table, s->bin_count, s->bin_start,
+            s->sb_start, (const T*)s->recs1, (T*)s->recs);
 }
 
 #define SDP_ES_BY_THREADS(NTV, CALL) \
@@ -1793,11 +2098,19 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
     sdp_Error st = SDP_SUCCESS;
     sdp_Error* status = &st;
     const int64_t num_vis = num_rows * num_chan;
-    const int nc = num_chunks(num_vis, p.nbins);
+    const int nc = num_chunks(num_vis, p.tstride);
     const int64_t chunk = (num_rows + nc - 1) / nc;   // rows per chunk
     const int passes = (p.nbins + kBinsPerPass - 1) / kBinsPerPass;
     const dim3 grid_b(nc, passes);
     const int nt = bucket_threads();
+    if (p.nsbins < 1 || p.nsbins > kMaxSuperBins ||
+            (1 << (2 * p.sshift)) > kMaxSuperTiles ||
+            p.tstride != p.nbins + p.nsbins ||
+            (size_t)nc * p.tstride > s->table_entries)
+    {
+        SDP_LOG_ERROR("Bucketing geometry / count table mismatch");
+        return SDP_ERR_RUNTIME;
+    }
     if (mode == MODE_GRID)
         SDP_ES_BY_THREADS(nt, (launch_count<T, MODE_GRID, NT>(grid_b, p,
                 num_rows, num_chan, chunk, uvw, freq, s->table, stream)))
@@ -1805,8 +2118,9 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
         SDP_ES_BY_THREADS(nt, (launch_count<T, MODE_DEGRID, NT>(grid_b, p,
                 num_rows, num_chan, chunk, uvw, freq, s->table, stream)))
     SDP_HIP_CHECK_LAUNCH(status);
-    k_scan_columns<<<(p.nbins + 63) / 64, 1024, 0, stream>>>(
-            s->table, nc, p.nbins, s->bin_count);
+    // Tile and super-bin columns of the count table in one launch.
+    k_scan_columns<<<(p.tstride + 63) / 64, 1024, 0, stream>>>(
+            s->table, nc, p.tstride, s->bin_count);
     SDP_HIP_CHECK_LAUNCH(status);
     k_scan_bins<<<1, 1024, 0, stream>>>(s->bin_count, p.nbins,
             s->bin_start, s->item_start, s->totals, s->item_bin,
@@ -1817,7 +2131,7 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
     const int words = (mode == MODE_GRID && p.do_w) ? 8 : 4;
     const size_t worst = (size_t)num_vis * (mode == MODE_GRID ? 4 : 1) *
             words * sizeof(T);
-    if (worst > s->recs_bytes)
+    if (worst > s->recs_bytes || (worst && !s->recs1))
     {
         SDP_LOG_ERROR("Bucketing scratch too small (%zu < %zu bytes)",
                 s->recs_bytes, worst);
@@ -1825,23 +2139,22 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
     }
     *n_entries = 0;                  // not known on the host
     *n_items = s->item_capacity;     // upper bound; extra items exit
-    T* recs = (T*)s->recs;
     if (mode == MODE_GRID)
     {
         if (p.do_w)
-            SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_GRID, true, NT>(grid_b,
-                    p, num_rows, num_chan, chunk, uvw, freq, vis, weight,
-                    s->table, s->bin_start, recs, stream)))
+            SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_GRID, true, NT>(nc,
+                    chunk, p, num_rows, num_chan, uvw, freq, vis, weight, s,
+                    stream)))
         else
-            SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_GRID, false, NT>(grid_b,
-                    p, num_rows, num_chan, chunk, uvw, freq, vis, weight,
-                    s->table, s->bin_start, recs, stream)))
+            SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_GRID, false, NT>(nc,
+                    chunk, p, num_rows, num_chan, uvw, freq, vis, weight, s,
+                    stream)))
     }
     else
     {
-        SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_DEGRID, false, NT>(grid_b,
-                p, num_rows, num_chan, chunk, uvw, freq, vis, weight,
-                s->table, s->bin_start, recs, stream)))
+        SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_DEGRID, false, NT>(nc,
+                chunk, p, num_rows, num_chan, uvw, freq, vis, weight, s,
+                stream)))
     }
     SDP_HIP_CHECK_LAUNCH(status);
     return *status;

@@ -54,6 +54,7 @@ struct sdp_GridderUvwEsFft
     int ncoarse;
     int ncbins;
     int nbins;
+    int sshift, nsuper, nsbins, tstride;    // super bins (bucketing level 1)
     sdp_es::BucketScratch scratch;
     sdp_fft::Plan2D* fft;       // rocFFT (f64, or grids es_fft does not take)
     int fused_fft;              // f32 power-of-two grid: pruned fused passes
@@ -216,10 +217,14 @@ void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
     {
         if (s.recs) SDP_HIP_CHECK(hipFree(s.recs), status);
         s.recs = nullptr;
+        if (s.recs1) SDP_HIP_CHECK(hipFree(s.recs1), status);
+        s.recs1 = nullptr;
         SDP_HIP_CHECK(hipMalloc(&s.recs, rec_bytes), status);
+        SDP_HIP_CHECK(hipMalloc(&s.recs1, rec_bytes), status);
         s.recs_bytes = *status ? 0 : rec_bytes;
     }
-    const size_t need = (size_t)sdp_es::num_chunks(num_vis, plan->nbins) * plan->nbins;
+    const size_t need = (size_t)sdp_es::num_chunks(num_vis, plan->tstride) *
+            plan->tstride;
     if (need > s.table_entries)
     {
         if (s.table) SDP_HIP_CHECK(hipFree(s.table), status);
@@ -264,6 +269,10 @@ sdp_es::EsParams<T> es_params(const sdp_GridderUvwEsFft* plan, int plane)
     p.ncoarse = plan->ncoarse;
     p.ncbins = plan->ncbins;
     p.nbins = plan->nbins;
+    p.sshift = plan->sshift;
+    p.nsuper = plan->nsuper;
+    p.nsbins = plan->nsbins;
+    p.tstride = plan->tstride;
     p.beta = (T)plan->beta;
     p.uv_scale = (T)plan->uv_scale;
     p.w_scale = (T)plan->w_scale;
@@ -468,6 +477,7 @@ void sdp_gridder_uvw_es_fft_free_plan(sdp_GridderUvwEsFft* plan)
     if (s.item_bin) (void)hipFree(s.item_bin);
     if (s.bin_count) (void)hipFree(s.bin_count);
     if (s.recs) (void)hipFree(s.recs);
+    if (s.recs1) (void)hipFree(s.recs1);
     sdp_fft::destroy_2d(plan->fft);
     sdp_es::fft_twiddles_destroy(&plan->fft_tw);
     if (plan->timing)
@@ -554,6 +564,17 @@ sdp_GridderUvwEsFft* sdp_gridder_uvw_es_fft_create_plan(
     plan->ncbins = plan->ncoarse * plan->ncoarse;
     plan->nbins = plan->ncbins * sdp_es::kCoarse * sdp_es::kCoarse;
     plan->stream = 0;
+    if (!sdp_es::super_geometry(plan->ntiles, &plan->sshift, &plan->nsuper,
+            &plan->nsbins))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Grid size %d too large for the bucketing",
+                plan->grid_size);
+        free(host);
+        sdp_gridder_uvw_es_fft_free_plan(plan);
+        return nullptr;
+    }
+    plan->tstride = plan->nbins + plan->nsbins;
 
     if (!sdp_hip::device_available())
     {
@@ -590,14 +611,17 @@ sdp_GridderUvwEsFft* sdp_gridder_uvw_es_fft_create_plan(
     const size_t nb = (size_t)plan->nbins;
     if (!*status)
     {
-        // bin_count | bin_start | item_start | totals in one allocation.
+        // bin_count (tile then super-bin totals) | bin_start | item_start |
+        // totals in one allocation.
         SDP_HIP_CHECK(hipMalloc(&s.bin_count,
-                (nb + 2 * (nb + 1) + 2) * sizeof(uint32_t)), status);
+                (plan->tstride + 2 * (nb + 1) + 2 + plan->nsbins + 1) *
+                sizeof(uint32_t)), status);
         if (!*status)
         {
-            s.bin_start = s.bin_count + nb;
+            s.bin_start = s.bin_count + plan->tstride;
             s.item_start = s.bin_start + nb + 1;
             s.totals = s.item_start + nb + 1;
+            s.sb_start = s.totals + 2;
         }
     }
     ensure_scratch(plan,
