@@ -6,7 +6,7 @@ import sys
 KEYS = ["k_bucket_fill1<float, 0", "k_bucket_fill2<float, 0",
         "k_bucket_fill1<float, 1", "k_bucket_fill2<float, 1",
         "k_bucket_count<float, 0", "k_bucket_count<float, 1",
-        "k_scan_columns", "k_scan_bins", "k_scatter_tab", "k_gather_tab"]
+        "k_scan_columns", "k_scan_bins", "k_scatter_tab", "k_scatter_pad", "k_gather_tab"]
 out = sys.argv[1]
 for n in sys.argv[2:]:
     fs = glob.glob(f"{out}/{n}/**/*kernel_stats.csv", recursive=True)

@@ -1176,14 +1176,21 @@ __device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
 // waves of 16-row bands each holding four sub-tiles' re / im in MFMA
 // accumulators: the tile's update is a sum of rank-1 outer products
 // ku (x) (kv w V), applied four visibilities per v_mfma_f32_16x16x4_f32.
-// The ES taps are evaluated ONCE per bucketed entry: at staging, thread t
-// evaluates the NTAP u-taps (checkerboard sign folded in) and the NTAP
-// v-taps times the weighted visibility of its entry into LDS tables. A visit is a packed 32-bit
-// {entry, u0 - tile row + 32, v0 - tile col + 32} word. Per chunk: the
-// next chunk's records are prefetched, the pool is laid out without
-// atomics (pool_count / pool_layout), three barriers, and the MFMA loop
-// issues all LDS reads of four groups before the matrix ops.
-template<bool DO_W, int NTAP>
+// The ES taps are evaluated ONCE per bucketed entry, in chunks of CHUNK =
+// 128 entries: thread t < 128 evaluates entry t's NTAP u-taps, thread
+// t + 128 its v-taps times the weighted visibility (checkerboard signs
+// folded in), each with its own axis's tap range, band mask and table
+// position. The tables are zero-padded: entry e's taps sit at kLead +
+// e * kStride in rows of NTAP + 15 slots whose tail (and the lead before
+// entry 0) stays zero, so the 16 rows (columns) of a sub-tile read taps
+// d0 + i, d0 in [-15, NTAP), with no range check. A visit is one word
+// {u index of row 0, v index of column 0}: the entry's word plus a
+// per-(band, column block) constant, written by ballot compaction into
+// the wave's list of each column block, and the matrix loop spends two
+// vector operations per operand. Barriers are LDS-only and the next
+// chunk's records load after this chunk's staging (no s_waitcnt vmcnt
+// before the visit loops).
+template<bool DO_W, int NTAP, int CHUNK = 128>
 __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
@@ -1191,40 +1198,42 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         int skip_empty)
 {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    constexpr int kChunk = 256;           // one entry per thread
-    constexpr int kVec = DO_W ? 2 : 1;    // float4s per bucketed record
-    // Per-wave visit lists: wave w, column block c holds the chunk's
-    // entries whose taps touch sub-tile (w, c), in entry order.
-    __shared__ uint16_t s_list[4][4][kChunk];
-    // Packed entry + hit masks; slot kChunk is the padding visit, whose
-    // offsets put every lane's tap index out of range (zero taps).
-    __shared__ uint32_t s_info[kChunk + 1];
-    // Tap tables; the extra last element of each is a zero that masked
-    // lanes read instead of branching around the load.
-    constexpr int kZero = kChunk * NTAP;
-    __shared__ float s_ku[kChunk * NTAP + 1];     // signed u-taps per entry
-    __shared__ float2 s_kv[kChunk * NTAP + 1];    // signed v-taps x w V
+    static_assert(CHUNK == 128 || CHUNK == 256, "one or two threads per entry");
+    constexpr int kVec = DO_W ? 2 : 1;
+    constexpr int kStride = NTAP + 15;
+    constexpr int kLead = 16;
+    constexpr int kTab = kLead + CHUNK * kStride;
+    static_assert(kTab < 65536, "16-bit table indices");
+    __shared__ float s_ku[kTab];
+    __shared__ float2 s_kv[kTab];
+    __shared__ uint32_t s_list[4][CHUNK + 4];
+    // Per entry: byte 0 = row bands hit, byte 1 = column blocks hit (0 for
+    // entries past the chunk); s_pos: table index of the entry's row 0 /
+    // column 0 of the tile, + 64 (lo: u, hi: v). With CHUNK = 128 the u
+    // half and the v half of both are written by the entry's two threads.
+    __shared__ uint32_t s_info[CHUNK];
+    __shared__ uint32_t s_pos[CHUNK];
 
     const uint32_t item = blockIdx.x;
-    if (item_bin[item] == kNoBin) return;   // past the last work item
+    if (item_bin[item] == kNoBin) return;
     const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
     const uint32_t npieces = item_start[b + 1] - item_start[b];
     const uint32_t e0 = bin_start[b] + piece * kPiece;
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
-    // An empty tile is left unwritten when its only reader, the fused FFT
-    // row pass, is told (from the bin counts) to take it as zeros.
     if (skip_empty && e0 == e1 && npieces == 1) return;
-    const int half = p.G / 2;
     int r0, c0;
     tile_origin(p, b, r0, c0);
-    if (r0 >= p.G || c0 >= p.G) return;    // phantom tile
+    if (r0 >= p.G || c0 >= p.G) return;
+    const int half = p.G / 2;
     const int tu0 = r0 - half, tv0 = c0 - half;
     const int t = threadIdx.x;
     const int lane = t & 63, wave = t >> 6;
     const int i = lane & 15, kq = lane >> 4;
-    const int sub_r = wave * 16;           // this wave's row band
-    const int base_u = sub_r + i + 32;     // tap index = base_u - packed ou
+    const int sub_r = wave * 16;
+    const int et = t & (CHUNK - 1);               // this thread's entry
+    const bool stage_u = CHUNK == 256 || t < CHUNK;
+    const bool stage_v = CHUNK == 256 || t >= CHUNK;
     f32x4 acc_re[4], acc_im[4];
 #pragma unroll
     for (int cblk = 0; cblk < 4; ++cblk)
@@ -1232,33 +1241,29 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         acc_re[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         acc_im[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     }
-    if (t == 0)
+    for (int k = t; k < kTab; k += 256)
     {
-        s_ku[kZero] = 0.0f;
-        s_kv[kZero] = make_float2(0.0f, 0.0f);
-        s_info[kChunk] = 255u << 8 | 255u << 16;
+        s_ku[k] = 0.0f;
+        s_kv[k] = make_float2(0.0f, 0.0f);
     }
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rw = r;
-    if (e0 + t < e1)
+    if (e0 + et < e1)
     {
-        r = recs4[(size_t)(e0 + t) * kVec];
-        if (DO_W) rw = recs4[(size_t)(e0 + t) * kVec + 1];
+        r = recs4[(size_t)(e0 + et) * kVec];
+        if (DO_W) rw = recs4[(size_t)(e0 + et) * kVec + 1];
     }
-
-    for (uint32_t cb = e0; cb < e1; cb += kChunk)
+    for (uint32_t cb = e0; cb < e1; cb += CHUNK)
     {
-        const int n = (int)min((uint32_t)kChunk, e1 - cb);
-        float4 rn = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rwn = rn;
-        if (cb + kChunk + t < e1)   // prefetch the next chunk
-        {
-            rn = recs4[(size_t)(cb + kChunk + t) * kVec];
-            if (DO_W) rwn = recs4[(size_t)(cb + kChunk + t) * kVec + 1];
-        }
-        int wlo_r = 1, whi_r = 0, wlo_c = 1, whi_c = 0;
+        const int n = (int)min((uint32_t)CHUNK, e1 - cb);
+        // Tap range of this thread's axis (both with CHUNK = 256): same
+        // formula as tap_range / footprint.
+        const float hs = (float)p.support / 2.0f;
+        const int gmin = -p.G / 2, gmax = (p.G - 1) / 2;
+        const bool live = et < n;
         int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
-        uint32_t pk = 0;
-        if (t < n)
+        uint32_t rm = 0, cm = 0, pu16 = 0, pv16 = 0;
+        const int eb = kLead + et * kStride;
         {
 #pragma clang fp contract(off)
             if (DO_W)
@@ -1266,137 +1271,142 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 r.z *= rw.x;
                 r.w *= rw.x;
             }
-            tap_range(p, r.x, r.y, u0, u1, v0, v1);
-            wlo_r = max(u0 - tu0, 0) >> 4;
-            whi_r = min(u1 - tu0, kTile - 1) >> 4;
-            wlo_c = max(v0 - tv0, 0) >> 4;
-            whi_c = min(v1 - tv0, kTile - 1) >> 4;
-            // bits 24-27: row bands hit, 28-31: column blocks hit
-            const uint32_t rm = (2u << whi_r) - (1u << wlo_r);
-            const uint32_t cm = (2u << whi_c) - (1u << wlo_c);
-            pk = (uint32_t)t | (uint32_t)(u0 - tu0 + 32) << 8 |
-                    (uint32_t)(v0 - tv0 + 32) << 16 | rm << 24 | cm << 28;
+            u0 = max((int)ceilf(r.x - hs), gmin);
+            if (stage_u)
+            {
+                u1 = min((int)floorf(r.x + hs), gmax);
+                const int lo = max(u0 - tu0, 0) >> 4;
+                const int hi = min(u1 - tu0, kTile - 1) >> 4;
+                rm = live ? (2u << hi) - (1u << lo) : 0u;
+                pu16 = (uint32_t)(eb + 64 - (u0 - tu0));
+            }
+            if (stage_v)
+            {
+                v0 = max((int)ceilf(r.y - hs), gmin);
+                v1 = min((int)floorf(r.y + hs), gmax);
+                const int lo = max(v0 - tv0, 0) >> 4;
+                const int hi = min(v1 - tv0, kTile - 1) >> 4;
+                cm = live ? (2u << hi) - (1u << lo) : 0u;
+                pv16 = (uint32_t)(eb + 64 - (v0 - tv0));
+            }
         }
-        __syncthreads();   // B1: previous chunk's tables consumed
-        s_info[t] = pk;
-        if (t < n)
+        lds_barrier();   // B1: previous chunk's tables and lists consumed
+        if (CHUNK == 256)
+        {
+            s_info[et] = rm | cm << 8;
+            s_pos[et] = pu16 | pv16 << 16;
+        }
+        else
+        {
+            uint8_t* info8 = (uint8_t*)s_info;
+            uint16_t* pos16 = (uint16_t*)s_pos;
+            info8[4 * et + (stage_u ? 0 : 1)] = (uint8_t)(stage_u ? rm : cm);
+            pos16[2 * et + (stage_u ? 0 : 1)] = (uint16_t)(stage_u ? pu16 : pv16);
+        }
+        if (live)
         {
 #pragma clang fp contract(off)
-            float tu[NTAP], tv[NTAP];
-            axis_taps<NTAP, true>(p, r.x, u0, u1, tu);
-            axis_taps<NTAP, true>(p, r.y, v0, v1, tv);
-            // (-1)^(u0 + v0) of the checkerboard, on the weighted
-            // visibility (sign flips: the products are unchanged)
-            const bool neg = ((u0 + v0) & 1) != 0;
-            const float zr = neg ? -r.z : r.z, zi = neg ? -r.w : r.w;
-#pragma unroll
-            for (int d = 0; d < NTAP; ++d)
+            if (stage_u)
             {
-                s_ku[t * NTAP + d] = tu[d];
-                s_kv[t * NTAP + d] = make_float2(tv[d] * zr, tv[d] * zi);
+                float tu[NTAP];
+                axis_taps<NTAP, true>(p, r.x, u0, u1, tu);
+#pragma unroll
+                for (int d = 0; d < NTAP; ++d) s_ku[eb + d] = tu[d];
+            }
+            if (stage_v)
+            {
+                float tv[NTAP];
+                axis_taps<NTAP, true>(p, r.y, v0, v1, tv);
+                const bool neg = ((u0 + v0) & 1) != 0;
+                const float zr = neg ? -r.z : r.z, zi = neg ? -r.w : r.w;
+#pragma unroll
+                for (int d = 0; d < NTAP; ++d)
+                    s_kv[eb + d] = make_float2(tv[d] * zr, tv[d] * zi);
             }
         }
-        __syncthreads();   // B2: entry info and tap tables complete
-        // This wave's visit lists (deterministic: entry order), by ballot
-        // compaction over the chunk's entries.
-        int lcnt[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int gi = 0; gi < 4; ++gi)
+        // Next chunk's records, issued after this chunk's last use of r so
+        // that nothing waits for them before the next staging.
+        if (cb + CHUNK + et < e1)
         {
-            const uint32_t info = s_info[gi * 64 + lane];
-            const bool in_band = (info >> (24 + wave)) & 1u;
+            r = recs4[(size_t)(cb + CHUNK + et) * kVec];
+            if (DO_W) rw = recs4[(size_t)(cb + CHUNK + et) * kVec + 1];
+        }
+        lds_barrier();   // B2: entry words and tap tables complete
+        uint32_t* list = s_list[wave];
+        // The chunk's entry words, read once for the four column blocks.
+        uint32_t inf[CHUNK / 64], ps[CHUNK / 64];
 #pragma unroll
-            for (int cblk = 0; cblk < 4; ++cblk)
+        for (int gi = 0; gi < CHUNK / 64; ++gi)
+        {
+            inf[gi] = s_info[gi * 64 + lane];
+            ps[gi] = s_pos[gi * 64 + lane];
+        }
+        const uint64_t below = (1ull << lane) - 1ull;
+#pragma unroll
+        for (int cblk = 0; cblk < 4; ++cblk)
+        {
+            // This wave's visits of sub-tile (wave, cblk), in entry order.
+            // Visit word = entry word + (sub_r - 64, cblk * 16 - 64): both
+            // halves stay non-negative for a visited sub-tile, so the one
+            // 32-bit add does not carry between them.
+            const uint32_t kadd = (uint32_t)(sub_r - 64) +
+                    ((uint32_t)(cblk * 16 - 64) << 16);
+            int cnt = 0;
+#pragma unroll
+            for (int gi = 0; gi < CHUNK / 64; ++gi)
             {
-                const bool hit = in_band && ((info >> (28 + cblk)) & 1u);
+                const bool hit = (inf[gi] >> wave) & (inf[gi] >> (8 + cblk)) & 1u;
                 const uint64_t m = __ballot(hit);
-                const int pos = lcnt[cblk] +
-                        (int)__popcll(m & ((1ull << lane) - 1ull));
-                if (hit) s_list[wave][cblk][pos] = (uint16_t)(info & 0xffu);
-                lcnt[cblk] += (int)__popcll(m);
+                if (hit)
+                    list[cnt + (int)__popcll(m & below)] = ps[gi] + kadd;
+                cnt += (int)__popcll(m);
             }
-        }
-        // Pad every list to a multiple of 4 visits (one matrix op) with the
-        // padding visit, so the matrix loop needs no bounds checks.
-#pragma unroll
-        for (int cblk = 0; cblk < 4; ++cblk)
-        {
-            const int pad = ((lcnt[cblk] + 3) & ~3) - lcnt[cblk];
-            if (lane < pad) s_list[wave][cblk][lcnt[cblk] + lane] = kChunk;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int cblk = 0; cblk < 4; ++cblk)
-        {
-            const int cnt4 = __builtin_amdgcn_readfirstlane(
-                    (lcnt[cblk] + 3) & ~3);
-            const int cnt = cnt4 & ~15;
-            const uint16_t* list = s_list[wave][cblk];
-            const int base_v = cblk * 16 + i + 32;
-            // The loop carries only this block's two accumulators (keeps
-            // the register allocator from rotating the AGPRs of all four).
+            const int cnt4 = (cnt + 3) & ~3;
+            if (lane < cnt4 - cnt) list[cnt + lane] = 0u;   // zero visit
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            const int n4 = __builtin_amdgcn_readfirstlane(cnt4);
+            const int n16 = n4 & ~15;
             f32x4 re = acc_re[cblk], im = acc_im[cblk];
-            // Tail first: the last (cnt4 - cnt) / 4 groups of four visits,
-            // one matrix op each.
-            for (int g = cnt; g < cnt4; g += 4)
+            for (int g = n16; g < n4; g += 4)
             {
-                const uint32_t q = s_info[list[g + kq]];
-                const int e = (int)(q & 0xffu);
-                const int du = base_u - (int)((q >> 8) & 0xffu);
-                const int dv = base_v - (int)((q >> 16) & 0xffu);
-                const int ia = ((unsigned)du < (unsigned)NTAP) ?
-                        e * NTAP + du : kZero;
-                const int ib = ((unsigned)dv < (unsigned)NTAP) ?
-                        e * NTAP + dv : kZero;
-                const float a = s_ku[ia];
-                const float2 bb = s_kv[ib];
+                const uint32_t w = list[g + kq];
+                const float a = s_ku[(w & 0xffffu) + i];
+                const float2 bb = s_kv[(w >> 16) + i];
                 re = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.x, re, 0, 0, 0);
                 im = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.y, im, 0, 0, 0);
             }
-            // Four groups of four visits per step: all LDS reads of a step
-            // are issued before the first matrix op waits on them.
-            for (int g = 0; g < cnt; g += 16)
+            for (int g = 0; g < n16; g += 16)
             {
-                uint32_t q[4];
+                uint32_t w[4];
 #pragma unroll
-                for (int s = 0; s < 4; ++s)
-                    q[s] = s_info[list[g + 4 * s + kq]];
+                for (int s2 = 0; s2 < 4; ++s2) w[s2] = list[g + 4 * s2 + kq];
                 float a[4];
                 float2 bb[4];
 #pragma unroll
-                for (int s = 0; s < 4; ++s)
+                for (int s2 = 0; s2 < 4; ++s2)
                 {
-                    const int e = (int)(q[s] & 0xffu);
-                    const int du = base_u - (int)((q[s] >> 8) & 0xffu);
-                    const int dv = base_v - (int)((q[s] >> 16) & 0xffu);
-                    const int ia = ((unsigned)du < (unsigned)NTAP) ?
-                            e * NTAP + du : kZero;
-                    const int ib = ((unsigned)dv < (unsigned)NTAP) ?
-                            e * NTAP + dv : kZero;
-                    a[s] = s_ku[ia];
-                    bb[s] = s_kv[ib];
+                    a[s2] = s_ku[(w[s2] & 0xffffu) + i];
+                    bb[s2] = s_kv[(w[s2] >> 16) + i];
                 }
-                // Each chain back to back (same-accumulator MFMAs forward
-                // their result); interleaving re / im made the register
-                // allocator swap the two accumulators every iteration.
 #pragma unroll
-                for (int s = 0; s < 4; ++s)
-                    re = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bb[s].x,
+                for (int s2 = 0; s2 < 4; ++s2)
+                    re = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], bb[s2].x,
                             re, 0, 0, 0);
 #pragma unroll
-                for (int s = 0; s < 4; ++s)
-                    im = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bb[s].y,
+                for (int s2 = 0; s2 < 4; ++s2)
+                    im = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], bb[s2].y,
                             im, 0, 0, 0);
             }
             acc_re[cblk] = re;
             acc_im[cblk] = im;
+            // The list is rebuilt for the next column block.
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
         }
-        r = rn;
-        rw = rwn;
     }
-
-    // C/D layout of 16x16x4 f32: col = lane & 15, row = (lane >> 4)*4 + r.
 #pragma unroll
     for (int cblk = 0; cblk < 4; ++cblk)
     {

@@ -67,6 +67,9 @@ CASES = [
     # the arrays for them)
     (False, False, 140000, 64, 256, 1e-5),
     (False, True, 140000, 64, 256, 1e-5),
+    # f32 at eps 1e-7: W = 16, the 17-slot tap tables of the tile kernels
+    (False, False, 3000, 3, 256, 1e-7),
+    (False, True, 1500, 2, 256, 1e-7),
 ]
 
 
