@@ -897,7 +897,15 @@ __host__ __device__ constexpr int prep_stride(int W)
 #define TOWER_DFT_WAVES 4
 #endif
 #ifndef TOWER_IDFT_WAVES
-#define TOWER_IDFT_WAVES 4
+#define TOWER_IDFT_WAVES 6
+#endif
+// k_tower_idft: staged visibilities (ring) and w-layers between re-anchored
+// images (see k_tower_idft).
+#ifndef SDP_IDFT_CAP
+#define SDP_IDFT_CAP 16
+#endif
+#ifndef SDP_IDFT_BLOCK
+#define SDP_IDFT_BLOCK 16
 #endif
 constexpr int kDftCap = 32;      // staged visibilities (ring)
 constexpr int kDftTile = 32;     // tile edge (pixels)
@@ -929,8 +937,8 @@ struct DftParams
     float2* part;                   // degrid: [visibility][tile] partials
 };
 
-// Ring slots (x .. x + cnt) & (kDftCap - 1) <- records v0 .. v0 + cnt - 1.
-template<int KWN>
+// Ring slots (x .. x + cnt) & (CAP - 1) <- records v0 .. v0 + cnt - 1.
+template<int KWN, int CAP = kDftCap>
 __device__ __forceinline__ void stage_records(const DftParams& d, int64_t v0,
         int x, int cnt, int W, int t, int (*s_tap)[2], float2* s_V,
         float (*s_kuv)[32], float (*s_kw)[KWN])
@@ -941,7 +949,7 @@ __device__ __forceinline__ void stage_records(const DftParams& d, int64_t v0,
     for (int o = t; o < total; o += 256)
     {
         const int vi = o / stride, w = o - vi * stride;
-        const int rs = (x + vi) & (kDftCap - 1);
+        const int rs = (x + vi) & (CAP - 1);
         const float f = src[o];
         if (w < 2) s_tap[rs][w] = __float_as_int(f);
         else if (w < 4) continue;
@@ -1227,18 +1235,20 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
 {
 #pragma clang fp contract(off)
     constexpr int kCols = kDftTile * NB;             // tile columns
+    constexpr int kCap = SDP_IDFT_CAP, kBlk = SDP_IDFT_BLOCK;
+    static_assert((kCap & (kCap - 1)) == 0 && kCap >= 16, "ring of >= 16");
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     extern __shared__ float2 s_tw[];                // e^{2 pi i k / S}, S
     __shared__ int s_start[kDftLayers + 1];
     // Rows padded by 2 float2: a lane reads 4 consecutive entries of its
     // visibility's row (two 16-byte LDS reads) and the 16 lanes of a
     // quarter-wave, on 16 different rows, then cover all 64 banks once.
-    __shared__ float2 s_ku[kDftCap][kDftTile + 2];  // conj KU(l), tile rows
-    __shared__ float2 s_kv[kDftCap][kCols + 2];     // conj KV(m), tile cols
-    __shared__ float s_kw[kDftCap][17];             // keyed by w-layer % 16
-    __shared__ int s_tap[kDftCap][2];
-    __shared__ float s_kuv[kDftCap][32];
-    __shared__ float2 s_acc[4][kDftCap];            // per-wave partials
+    __shared__ float2 s_ku[kCap][kDftTile + 2];  // conj KU(l), tile rows
+    __shared__ float2 s_kv[kCap][kCols + 2];     // conj KV(m), tile cols
+    __shared__ float s_kw[kCap][17];             // keyed by w-layer % 16
+    __shared__ int s_tap[kCap][2];
+    __shared__ float s_kuv[kCap][32];
+    __shared__ float2 s_acc[4][kCap];            // per-wave partials
 
     const TowerParams& tp = d.tp;
     const int S = tp.S, ws = tp.w_support, W = tp.support;
@@ -1264,9 +1274,39 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
     // (MFMA kk takes its k = kq from column bm + 4 kq + kk; any bijection
     // of the 16 columns works as long as A and B share it, and this one
     // puts a lane's 4 B entries next to each other in LDS).
-    Cx<double> y64[NB][4], dinv_k[NB][4];
+    // Y_L = X D^-(L - w_support/2) is evaluated afresh from the sub-grid
+    // image every kBlk layers (anchor: X in double times the f32-accurate
+    // phase, as the reference's complex-double wimg to f32 accuracy) and
+    // carried in between by the f32 recurrence Y_{L+1} = Y_L / D (1 / D
+    // rounded to f32): no per-pixel double state stays in registers.
     float2 y32[NB][4], dinv32[NB][4];
     const Cx<float>* X = d.in + (int64_t)slot * S * S;
+    auto anchor = [&](int L) {
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+            {
+                const int pr = L0 + bl + i;
+                const int pc = M0 + kDftTile * nb + bm + 4 * kq + kk;
+                const int64_t e = (int64_t)pr * S + pc;
+                // Input checkerboard and 1 / S^2 of the sub-grid inverse
+                // FFT (.cpp:423-427), in single precision as the reference's
+                // layers.
+                Cx<float> x = X[e];
+                if ((pr + pc) & 1)
+                {
+                    x.re = -x.re;
+                    x.im = -x.im;
+                }
+                x.re *= d.norm;
+                x.im *= d.norm;
+                const Cx<double> y = cmul(cx<double>((double)x.re,
+                        (double)x.im), pattern_pow_f32(d.w_turns[e],
+                        -(L - ws / 2)));
+                y32[nb][kk] = make_float2((float)y.re, (float)y.im);
+            }
+    };
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
@@ -1274,28 +1314,13 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
         {
             const int pr = L0 + bl + i;
             const int pc = M0 + kDftTile * nb + bm + 4 * kq + kk;
-            const int64_t e = (int64_t)pr * S + pc;
-            // Input checkerboard and 1 / S^2 of the sub-grid inverse FFT
-            // (.cpp:423-427), in single precision as the reference's layers.
-            Cx<float> x = X[e];
-            if ((pr + pc) & 1)
-            {
-                x.re = -x.re;
-                x.im = -x.im;
-            }
-            x.re *= d.norm;
-            x.im *= d.norm;
-            y64[nb][kk] = cmul(cx<double>((double)x.re, (double)x.im),
-                    pattern_pow_f32(d.w_turns[e], -(L_first - ws / 2)));
-            const Cx<double> di = d.wp_inv[e];
+            const Cx<double> di = d.wp_inv[(int64_t)pr * S + pc];
             dinv32[nb][kk] = make_float2((float)di.re, (float)di.im);
-            dinv_k[nb][kk] = cpow_int(di, kDftBlock);
-            y32[nb][kk] = make_float2((float)y64[nb][kk].re,
-                    (float)y64[nb][kk].im);
         }
+    anchor(L_first);
     for (int k = t; k < S; k += 256) s_tw[k] = d.tw[k];
-    for (int k = t; k < 4 * kDftCap; k += 256)
-        s_acc[k / kDftCap][k & (kDftCap - 1)] = make_float2(0.0f, 0.0f);
+    for (int k = t; k < 4 * kCap; k += 256)
+        s_acc[k / kCap][k & (kCap - 1)] = make_float2(0.0f, 0.0f);
     if (t == 0)
     {
         s_start[0] = 0;
@@ -1321,7 +1346,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
     auto flush = [&](int f0, int f1) {
         for (int v = f0 + ((t - f0) % 256 + 256) % 256; v < f1; v += 256)
         {
-            const int rs = v & (kDftCap - 1);
+            const int rs = v & (kCap - 1);
             float2 sum = make_float2(0.0f, 0.0f);
 #pragma unroll
             for (int w = 0; w < 4; ++w)
@@ -1345,12 +1370,12 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
     {
         const int lo = s_start[max(0, min(npl, L - ws + 1 - P_first))];
         const int hi = s_start[max(0, min(npl, L + 1 - P_first))];
-        for (int a = lo; a < hi; a += kDftCap)
+        for (int a = lo; a < hi; a += kCap)
         {
-            const int b = min(hi, a + kDftCap);
+            const int b = min(hi, a + kCap);
             if (!(a >= st_lo && b <= st_hi))
             {
-                const int e = min(n, a + kDftCap);
+                const int e = min(n, a + kCap);
                 const bool keep = a >= st_lo && a <= st_hi;
                 const int x = keep ? st_hi : a;
                 lds_sync();   // all partials of the ring written
@@ -1359,14 +1384,14 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                 st_lo = a;
                 st_hi = e;
                 const int cnt = e - x;
-                stage_records(d, s0 + x, x, cnt, W, t, s_tap, nullptr, s_kuv,
-                        s_kw);
+                stage_records<17, kCap>(d, s0 + x, x, cnt, W, t, s_tap, nullptr,
+                        s_kuv, s_kw);
                 lds_sync();
                 constexpr int kPer = kDftTile + kCols;   // rows, columns
                 for (int o = t; o < cnt * kPer; o += 256)
                 {
                     const int v = x + (int)((unsigned)o / kPer);
-                    const int rs = v & (kDftCap - 1);
+                    const int rs = v & (kCap - 1);
                     const int q = (int)((unsigned)o % kPer);
                     const int iu0 = s_tap[rs][0];
                     float2 res = make_float2(0.0f, 0.0f);
@@ -1405,7 +1430,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                 const bool ok = v < b;
                 // Column i of T only sees column i of B: a lane past the
                 // window reads a staged row and its result is dropped below.
-                const int rs = (ok ? v : a) & (kDftCap - 1);
+                const int rs = (ok ? v : a) & (kCap - 1);
                 // Complex product in three real matrix products (Gauss):
                 // t1 = Yr Kr, t2 = Yi Ki, t3 = (Yr + Yi)(Kr + Ki), then
                 // T = (t1 - t2) + i (t3 - t1 - t2): 3 instead of 4 matrix
@@ -1465,17 +1490,9 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
             }
         }
         // Y_{L+1} = Y_L / D.
-        if ((L + 1 - L_first) % kDftBlock == 0)
+        if ((L + 1 - L_first) % kBlk == 0)
         {
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-                for (int kk = 0; kk < 4; ++kk)
-                {
-                    y64[nb][kk] = cmul(y64[nb][kk], dinv_k[nb][kk]);
-                    y32[nb][kk] = make_float2((float)y64[nb][kk].re,
-                            (float)y64[nb][kk].im);
-                }
+            if (L < L_last) anchor(L + 1);
         }
         else
         {
