@@ -39,9 +39,12 @@ namespace sdp_es {
 bool fused_fft_supported(int grid_size);
 
 // Twiddle table exp(-2 pi i m / G), m in [0, G), as float2 in device memory.
+// Also owns the occupied-tile bitmap of the real-output gridding row pass
+// (G / 64 tile rows of max(1, G / 4096) 64-bit words).
 struct FftTwiddles
 {
     void* table = nullptr;
+    void* masks = nullptr;
     int G = 0;
 };
 int fft_twiddles_create(int grid_size, FftTwiddles* tw);

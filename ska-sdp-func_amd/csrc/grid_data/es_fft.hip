@@ -723,6 +723,255 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
     }
 }
 
+// Gridding, 2-D: the real-output form ---------------------------------------
+//
+// The 2-D gridder keeps only Re of the transform (checkerboard and
+// correction are real), and Re(IDFT2(A)) = IDFT2(H) with the Hermitian part
+// H[u][v] = (A[u][v] + conj(A[-u][-v])) / 2 (indices mod G). The row
+// transforms Bh[u][x] of H are Hermitian down every column (Bh[-u][x] =
+// conj(Bh[u][x])), so the column transform is complex-to-real: with
+// Xe[k] = Bh[k] + conj(Bh[G/2 - k]) and Xo[k] = (Bh[k] - conj(Bh[G/2 - k]))
+// e^{2 pi i k / G}, the length-G/2 transform z of Z = Xe + i Xo gives the
+// output rows 2m (Re z[m]) and 2m + 1 (Im z[m]). The row pass forms Z
+// directly: one workgroup per quad of grid rows {k, G - k, G/2 - k,
+// G/2 + k} (k = 0: {0, G/2}; k = G/4: {G/4, 3G/4}; the quads partition the
+// rows, so the pass stays in place) transforms the H rows k and G/2 - k and
+// writes the Z rows k and G/2 - k. The column passes then move G/2 rows
+// instead of G and the row pass writes half as much: ~1.3 GB of HBM
+// traffic per call at config 2 instead of ~2.0 GB, and half the column
+// FFT work.
+
+// Split of the half-length column transform, G2 = N1 * N2.
+template<int G2> struct HalfSplit;
+template<> struct HalfSplit<1024> { static constexpr int N1 = 32, N2 = 32; };
+template<> struct HalfSplit<2048> { static constexpr int N1 = 32, N2 = 64; };
+template<> struct HalfSplit<4096> { static constexpr int N1 = 64, N2 = 64; };
+template<> struct HalfSplit<8192> { static constexpr int N1 = 64, N2 = 128; };
+
+__host__ __device__ constexpr int mask_words(int G)
+{
+    return G / 64 > 64 ? G / 4096 : 1;
+}
+
+// Occupied-tile bitmap: word w of tile row tu has bit b set if tile
+// 64 w + b of that row holds bucketed entries (one 64-thread block per
+// tile row).
+__global__ void __launch_bounds__(64) k_tile_masks(
+        const uint32_t* __restrict__ tiles, int ncoarse, int ntiles,
+        int words, uint64_t* __restrict__ masks)
+{
+    const unsigned tu = blockIdx.x;
+    for (int w = 0; w < words; ++w)
+    {
+        const unsigned tv = (unsigned)(64 * w) + threadIdx.x;
+        bool occ = false;
+        if (tv < (unsigned)ntiles)
+        {
+            const unsigned bin = (((tu >> 2) * (unsigned)ncoarse + (tv >> 2))
+                    << 4) | ((tu & 3u) << 2) | (tv & 3u);
+            occ = tiles[bin] != 0u;
+        }
+        const uint64_t m = __ballot(occ);
+        if (threadIdx.x == 0) masks[tu * words + w] = m;
+    }
+}
+
+template<int G>
+__global__ void __launch_bounds__(RowPlan<G>::P)
+k_rows_herm(float2* __restrict__ grid, int k0, int M,
+        const float2* __restrict__ W, const uint64_t* __restrict__ masks)
+{
+    using F = RowFft<G, 1>;
+    constexpr int EPT = F::EPT, NW = mask_words(G), NQ = G / 4 + 1;
+    extern __shared__ float2 lds[];
+    const int p = threadIdx.x;
+    const Buf gb(grid - k0, grid_bytes(G, k0));
+    F f;
+    f.init(p, W, G);
+    const int per = (NQ + gridDim.x - 1) / gridDim.x;
+    const int q_begin = blockIdx.x * per, q_end = min(NQ, q_begin + per);
+    // H row u from grid rows u and -u (element v and -v); tiles with no
+    // bucketed entry were not written by the scatter and read as zero.
+    auto load_h = [&](float2 (&v)[EPT], int u, int pq) {
+        const int ur = (G - u) & (G - 1);
+        uint64_t wa[NW], wb[NW];
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+        {
+            wa[w] = masks ? masks[(u >> 6) * NW + w] : ~0ull;
+            wb[w] = masks ? masks[(ur >> 6) * NW + w] : ~0ull;
+        }
+        const uint32_t ra = ((uint32_t)u * G + k0) * 8u;
+        const uint32_t rb = ((uint32_t)ur * G + k0) * 8u;
+        F::load_input(v, [&](int c) {
+            const int ca = pq + c, cb = (G - ca) & (G - 1);
+            const int ta = ca >> 6, tb = cb >> 6;
+            const bool oa = (wa[NW > 1 ? ta >> 6 : 0] >> (ta & 63)) & 1ull;
+            const bool ob = (wb[NW > 1 ? tb >> 6 : 0] >> (tb & 63)) & 1ull;
+            const float2 a = gb.load_if(oa, ra + (uint32_t)ca * 8u);
+            const float2 b = gb.load_if(ob, rb + (uint32_t)cb * 8u);
+            return make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
+        });
+    };
+    for (int k = q_begin; k < q_end; ++k)
+    {
+        const int pq = opaque(p);
+        const int ub = G / 2 - k;              // == k for the quad k = G/4
+        float2 va[EPT], vb[EPT];
+        load_h(va, k, pq);
+        f.transform(va, pq, lds, RowIdx{});
+        if (ub != k)
+        {
+            load_h(vb, ub, pq);
+            f.transform(vb, pq, lds, RowIdx{});
+        }
+        else
+        {
+#pragma unroll
+            for (int i = 0; i < EPT; ++i) vb[i] = va[i];
+        }
+        // e^{2 pi i k / G} = conj(W[k]); e^{2 pi i (G/2 - k) / G} = -W[k].
+        const float2 wt = W[k];
+        const float2 wk = make_float2(wt.x, -wt.y);
+        const float2 wb = make_float2(-wt.x, -wt.y);
+        float2 za[EPT];
+#pragma unroll
+        for (int i = 0; i < EPT; ++i)
+        {
+            const float2 a = va[i], b = vb[i];
+            const float2 xe = make_float2(a.x + b.x, a.y - b.y);
+            const float2 xo = cmul(make_float2(a.x - b.x, a.y + b.y), wk);
+            za[i] = make_float2(xe.x - xo.y, xe.y + xo.x);
+            // Z[G/2 - k] from the same pair, roles swapped.
+            const float2 ye = make_float2(b.x + a.x, b.y - a.y);
+            const float2 yo = cmul(make_float2(b.x - a.x, b.y + a.y), wb);
+            vb[i] = make_float2(ye.x - yo.y, ye.y + yo.x);
+        }
+        const uint32_t vo = (uint32_t)pq * 8u;
+        const uint32_t va_row = (uint32_t)k * G * 8u + vo;
+        F::store_output(za, [&](int c, int, float2 x) {
+            gb.store_if((unsigned)(pq + c - k0) < (unsigned)M, x, va_row + c * 8u);
+        });
+        if (k > 0 && ub != k)
+        {
+            const uint32_t vb_row = (uint32_t)ub * G * 8u + vo;
+            F::store_output(vb, [&](int c, int, float2 x) {
+                gb.store_if((unsigned)(pq + c - k0) < (unsigned)M, x,
+                        vb_row + c * 8u);
+            });
+        }
+    }
+}
+
+// Column pass A of the half-length transform: for u1 = blockIdx.x,
+// length-N2 FFTs over the Z rows u1 + N1 * n2 (row pitch G = 2 N1 N2),
+// times e^{2 pi i u1 k2 / (G/2)}, back into rows u1 + N1 * k2.
+template<int N1, int N2>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_COLA_WAVES)))
+k_cols_a_herm(float2* __restrict__ grid, int M, const float2* __restrict__ W)
+{
+    constexpr int G = 2 * N1 * N2, B = ColPlan<N2>::B;
+    using F = ColFft<N2, 1>;
+    extern __shared__ float2 lds[];
+    const int c = threadIdx.x % B, p = threadIdx.x / B;
+    const int u1 = blockIdx.x;
+    const Buf gb(grid, grid_bytes(G, 0));
+    F f;
+    f.init(p, W, G);
+    float2 fs[F::EPT];
+#pragma unroll
+    for (int i = 0; i < F::EPT; ++i)
+        fs[i] = F::twiddle(W, 2 * u1 * F::out_index(p, i));
+    const int ncb = (M + B - 1) / B;
+    const uint32_t so = (uint32_t)u1 * G * 8u;
+    constexpr uint32_t kStep = (uint32_t)N1 * G * 8u;
+    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
+    {
+        const int pq = opaque(p), cq = opaque(c);
+        const int col = cb * B + cq;
+        const bool ok = col < M;
+        const uint32_t vo = ((uint32_t)pq * N1 * G + col) * 8u;
+        float2 v[F::EPT];
+        F::load_input(v, [&](int e) {
+            return ok ? gb.load(vo, so + e * kStep) : make_float2(0.f, 0.f);
+        });
+        f.transform(v, pq, lds, ColIdx<B>{cq});
+        F::store_output(v, [&](int e, int i, float2 x) {
+            if (ok) gb.store(cmul(x, fs[i]), vo, so + e * kStep);
+        });
+    }
+}
+
+// Column pass B of the half-length transform + 2-D image epilogue: for
+// k2 = blockIdx.x, length-N1 FFTs over rows N1 * k2 + n1; z[m], m = k2 +
+// N2 * k1, is Re: output row 2m, Im: output row 2m + 1 (image rows minus
+// k0), each then as k_cols_b_grid: dirty = (dirty + checker * f) /
+// correction.
+template<int N1, int N2>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_COLB_WAVES)))
+k_cols_b_herm(const float2* __restrict__ grid, float* __restrict__ dirty,
+        ImageParams<float> ip, int k0, int M, const float2* __restrict__ W)
+{
+#pragma clang fp contract(off)
+    constexpr int G = 2 * N1 * N2, B = ColPlan<N1>::B;
+    using F = ColFft<N1, 1>;
+    extern __shared__ float2 lds[];
+    const int c = threadIdx.x % B, p = threadIdx.x / B;
+    const int k2 = blockIdx.x;
+    const int h = M / 2;
+    const Buf gb(grid, grid_bytes(G, 0));
+    const BufF db(dirty, (uint32_t)((size_t)ip.N * ip.N * 4));
+    F f;
+    f.init(p, W, G);
+    const int ncb = (M + B - 1) / B;
+    const uint32_t so = (uint32_t)N1 * k2 * G * 8u;
+    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
+    {
+        const int pq = opaque(p), cq = opaque(c);
+        const int col = cb * B + cq;
+        const bool ok = col < M;
+        const uint32_t vo = ((uint32_t)pq * G + col) * 8u;
+        float2 v[F::EPT];
+        F::load_input(v, [&](int e) {
+            return ok ? gb.load(vo, so + e * (uint32_t)G * 8u)
+                      : make_float2(0.f, 0.f);
+        });
+        // The image values this thread adds to, loaded ahead of the
+        // transform (see k_cols_b_grid).
+        float prev[F::EPT][2];
+#pragma unroll
+        for (int i = 0; i < F::EPT; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+            {
+                const int iy = 2 * (k2 + N2 * F::out_index(pq, i)) + j - k0;
+                const bool in = ok && (unsigned)iy < (unsigned)M;
+                prev[i][j] = db.load_if(in, ((uint32_t)iy * ip.N + col) * 4u);
+            }
+        f.transform(v, pq, lds, ColIdx<B>{cq});
+        const float ccx = ip.conv_corr[min(abs(col - h), h)];
+        F::store_output(v, [&](int e, int i, float2 x) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+            {
+                const int iy = 2 * (k2 + N2 * (pq + e)) + j - k0;
+                const bool in = ok && (unsigned)iy < (unsigned)M;
+                const int ix = col;
+                const int yo = iy - h;
+                const uint32_t off = ((uint32_t)iy * ip.N + ix) * 4u;
+                float val = j ? x.y : x.x;
+                if ((ix + iy) & 1) val = -val;
+                float out = prev[i][j] + val;
+                // inv_correction (es_image_dev.h), 2-D branch, same order.
+                const float ccy = ip.conv_corr[min(abs(yo), h)];
+                const float corr = ccx * ccy * ip.norm * ip.norm;
+                out *= 1.0f / corr;
+                db.store_if(in, out, off);
+            }
+        });
+    }
+}
+
 // Column pass B in place (full 2-D FFTs of a whole grid, w-stacking): for
 // k2 = blockIdx.x, length-N1 FFTs over the contiguous rows N1 * k2 + n1,
 // output k1 back into row N1 * k2 + k1. Natural row k = k2 + N2 * k1 of the
@@ -1058,6 +1307,78 @@ int grid_to_image(const Geometry& g, const ImageParams<float>& ip, int plane,
     return st;
 }
 
+// Real-output (Hermitian) form of the 2-D gridding transform, for grids of
+// 2048 to 8192 (at 16384 the row pass's two 32-element rows per thread do
+// not fit the registers; env SDP_ES_HERM=0: the complex form, for A/B).
+bool herm_enabled(const ImageParams<float>& ip)
+{
+    static int on = -1;
+    if (on < 0)
+    {
+        const char* e = getenv("SDP_ES_HERM");
+        on = (e && e[0] == '0') ? 0 : 1;
+    }
+    return on && !ip.do_w && ip.G >= 2048 && ip.G <= 8192;
+}
+
+template<int N1, int N2>
+int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
+        const uint32_t* tiles, int ncoarse, uint64_t* masks,
+        hipStream_t stream)
+{
+    constexpr int G = N1 * N2;
+    if constexpr (G < 2048)
+    {
+        return SDP_ERR_INVALID_ARGUMENT;
+    }
+    else
+    {
+        using HS = HalfSplit<G / 2>;
+        sdp_Error st = SDP_SUCCESS;
+        if (tiles)
+        {
+            if (!masks) return SDP_ERR_RUNTIME;
+            k_tile_masks<<<G / 64, 64, 0, stream>>>(tiles, ncoarse, G / 64,
+                    mask_words(G), masks);
+            SDP_HIP_CHECK_LAUNCH(&st);
+            if (st) return st;
+        }
+        const size_t lds = row_lds_bytes(G);
+        SDP_HIP_CHECK((allow_lds<k_rows_herm<G>>(lds)), &st);
+        if (st) return st;
+        k_rows_herm<G><<<row_blocks(G), RowPlan<G>::P, lds, stream>>>(
+                grid, g.k0, g.M, W, tiles ? masks : nullptr);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        if (st) return st;
+        k_cols_a_herm<HS::N1, HS::N2><<<col_grid<k_cols_a_herm<HS::N1,
+                HS::N2>>(HS::N1, g.M, ColPlan<HS::N2>::B), 256, kColLdsBytes,
+                stream>>>(grid, g.M, W);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        return st;
+    }
+}
+
+template<int N1, int N2>
+int grid_to_image_herm(const Geometry& g, const ImageParams<float>& ip,
+        const float2* W, const float2* grid, float* dirty, hipStream_t stream)
+{
+    constexpr int G = N1 * N2;
+    if constexpr (G < 2048)
+    {
+        return SDP_ERR_INVALID_ARGUMENT;
+    }
+    else
+    {
+        using HS = HalfSplit<G / 2>;
+        sdp_Error st = SDP_SUCCESS;
+        k_cols_b_herm<HS::N1, HS::N2><<<col_grid<k_cols_b_herm<HS::N1,
+                HS::N2>>(HS::N2, g.M, ColPlan<HS::N1>::B), 256, kColLdsBytes,
+                stream>>>(grid, dirty, ip, g.k0, g.M, W);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        return st;
+    }
+}
+
 template<int N1, int N2>
 int image_cols(const Geometry& g, const ImageParams<float>& ip, int plane,
         const float2* W, float* dirty, bool correct, float2* grid,
@@ -1181,6 +1502,9 @@ int fft_twiddles_create(int grid_size, FftTwiddles* tw)
     if (st) return st;
     SDP_HIP_CHECK(hipMemcpy(tw->table, h.data(), h.size() * sizeof(float2),
             hipMemcpyHostToDevice), &st);
+    if (!st && grid_size >= 2048)
+        SDP_HIP_CHECK(hipMalloc(&tw->masks, (size_t)(grid_size / 64) *
+                mask_words(grid_size) * sizeof(uint64_t)), &st);
     tw->G = grid_size;
     return st;
 }
@@ -1188,7 +1512,9 @@ int fft_twiddles_create(int grid_size, FftTwiddles* tw)
 void fft_twiddles_destroy(FftTwiddles* tw)
 {
     if (tw->table) (void)hipFree(tw->table);
+    if (tw->masks) (void)hipFree(tw->masks);
     tw->table = nullptr;
+    tw->masks = nullptr;
     tw->G = 0;
 }
 
@@ -1197,6 +1523,9 @@ int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
 {
     const Geometry g = geometry(ip);
     const float2* W = (const float2*)tw.table;
+    if (herm_enabled(ip))
+        SDP_ES_FFT_DISPATCH(g.G, (grid_rows_cols_herm<N1, N2>(g, W,
+                (float2*)grid, tiles, ncoarse, (uint64_t*)tw.masks, stream)))
     SDP_ES_FFT_DISPATCH(g.G, (grid_rows_cols<N1, N2>(g, W, (float2*)grid,
             tiles, ncoarse, stream)))
 }
@@ -1206,6 +1535,9 @@ int fft_grid_to_image(const ImageParams<float>& ip, int plane,
 {
     const Geometry g = geometry(ip);
     const float2* W = (const float2*)tw.table;
+    if (herm_enabled(ip))
+        SDP_ES_FFT_DISPATCH(g.G, (grid_to_image_herm<N1, N2>(g, ip, W,
+                (const float2*)grid, dirty, stream)))
     SDP_ES_FFT_DISPATCH(g.G, (grid_to_image<N1, N2>(g, ip, plane, W,
             (const float2*)grid, dirty, stream)))
 }
