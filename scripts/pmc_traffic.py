@@ -24,9 +24,10 @@ PHASES = {
                     "k_scatter(", "k_gather_tab", "k_gather_mfma", "k_gather<",
                     "k_gather("),
     "image": ("k_screen_corr_2d", "k_screen_accumulate", "k_apply_correction",
-              "k_reverse_screen", "k_cols_b_grid"),
+              "k_reverse_screen", "k_cols_b_grid", "k_cols_b_herm"),
     # fused FFT passes (es_fft.hip); rocFFT kernels match "fft" below
-    "fft": ("k_rows_grid", "k_cols_a_grid"),
+    "fft": ("k_rows_grid", "k_cols_a_grid", "k_rows_herm", "k_cols_a_herm",
+            "k_row_occupancy"),
 }
 
 

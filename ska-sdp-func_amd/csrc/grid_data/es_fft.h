@@ -18,6 +18,13 @@
 //            the image with the screen + correction epilogue
 //            (2-D: dirty = (dirty + checker * Re) / correction;
 //             3-D: dirty += checker * Re(F * phasor(w)), per plane).
+//  2-D gridding with 2048 <= G <= 8192 takes the real-output form instead
+//   (es_fft.hip, k_rows_herm / k_cols_a_herm / k_cols_b_herm): the dirty
+//   image keeps only Re of the transform, so the row pass transforms the
+//   Hermitian part of the grid and packs each pair of row spectra into one
+//   row of a half-length complex-to-real column transform; the column
+//   passes move G/2 rows and the image row pairs 2m, 2m + 1 come from
+//   Re / Im of one output row.
 //  degridding (forward, -i): the mirror image -- the first column pass reads
 //   the (corrected in place) image with the checker / phasor prologue, the
 //   row pass zero-pads and writes every cell of the grid.
@@ -39,8 +46,8 @@ namespace sdp_es {
 bool fused_fft_supported(int grid_size);
 
 // Twiddle table exp(-2 pi i m / G), m in [0, G), as float2 in device memory.
-// Also owns the occupied-tile bitmap of the real-output gridding row pass
-// (G / 64 tile rows of max(1, G / 4096) 64-bit words).
+// Also owns the tile-occupancy table of the real-output gridding row pass
+// (G / 64 tile rows of G / 1024 + 1 32-bit words, es_fft.hip).
 struct FftTwiddles
 {
     void* table = nullptr;

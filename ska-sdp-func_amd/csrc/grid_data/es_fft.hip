@@ -746,120 +746,129 @@ template<int G2> struct HalfSplit;
 template<> struct HalfSplit<1024> { static constexpr int N1 = 32, N2 = 32; };
 template<> struct HalfSplit<2048> { static constexpr int N1 = 32, N2 = 64; };
 template<> struct HalfSplit<4096> { static constexpr int N1 = 64, N2 = 64; };
-template<> struct HalfSplit<8192> { static constexpr int N1 = 64, N2 = 128; };
 
-__host__ __device__ constexpr int mask_words(int G)
+// Occupancy of the row pass's loads. With P = G / 16 threads per row and
+// 16 elements each, thread p's element r of a row sits at column p + r P
+// (tile p / 64 + r S, S = P / 64) and its partner element at column
+// (G - p - r P) mod G (tile (T - ceil(p / 64) - r S) mod T, T = G / 64
+// tiles per row). So per tile row and thread class one 32-bit word holds
+// the 16 bits of both: low half forward (class p / 64), high half reversed
+// (class ceil(p / 64)), S + 1 classes.
+__host__ __device__ constexpr int occ_classes(int G)
 {
-    return G / 64 > 64 ? G / 4096 : 1;
+    return G / 1024 + 1;
 }
 
-// Occupied-tile bitmap: word w of tile row tu has bit b set if tile
-// 64 w + b of that row holds bucketed entries (one 64-thread block per
-// tile row).
-__global__ void __launch_bounds__(64) k_tile_masks(
-        const uint32_t* __restrict__ tiles, int ncoarse, int ntiles,
-        int words, uint64_t* __restrict__ masks)
+// One block per tile row, one thread per bit: thread t builds bit t % 32
+// of class t / 32's word (bits 0-15 forward, 16-31 reversed), and a wave's
+// ballot holds the words of two classes.
+// HALO (degridding): a tile counts if it or its upper / left / upper-left
+// neighbour holds entries (the gather's reach, as k_rows_image).
+template<bool HALO>
+__global__ void __launch_bounds__(320) k_row_occupancy(
+        const uint32_t* __restrict__ tiles, int ncoarse, int G,
+        uint32_t* __restrict__ occ)
 {
+    const int T = G / 64, S = G / 1024;
+    const int t = threadIdx.x, cls = t >> 5, j = t & 31, r = j & 15;
     const unsigned tu = blockIdx.x;
-    for (int w = 0; w < words; ++w)
+    int tv = -1;
+    if (cls <= S)
     {
-        const unsigned tv = (unsigned)(64 * w) + threadIdx.x;
-        bool occ = false;
-        if (tv < (unsigned)ntiles)
-        {
-            const unsigned bin = (((tu >> 2) * (unsigned)ncoarse + (tv >> 2))
-                    << 4) | ((tu & 3u) << 2) | (tv & 3u);
-            occ = tiles[bin] != 0u;
-        }
-        const uint64_t m = __ballot(occ);
-        if (threadIdx.x == 0) masks[tu * words + w] = m;
+        if (j < 16) tv = cls < S ? cls + r * S : -1;
+        else tv = ((T - cls - r * S) % T + T) % T;
     }
+    auto count = [&](int a, int b) -> uint32_t {
+        if (a < 0 || b < 0) return 0u;
+        const unsigned x = (unsigned)a, y = (unsigned)b;
+        return tiles[(((x >> 2) * (unsigned)ncoarse + (y >> 2)) << 4) |
+                ((x & 3u) << 2) | (y & 3u)];
+    };
+    bool bit = false;
+    if (tv >= 0)
+    {
+        const int a = (int)tu;
+        bit = HALO ? (count(a, tv) | count(a - 1, tv) | count(a, tv - 1) |
+                count(a - 1, tv - 1)) != 0u : count(a, tv) != 0u;
+    }
+    const uint64_t m = __ballot(bit);
+    if (j == 0 && cls <= S)
+        occ[tu * (S + 1) + cls] = (uint32_t)(m >> (t & 32));
 }
 
+// The two H rows of a quad are transformed side by side by the two halves
+// of the workgroup (each its own LDS row buffer), then swapped through LDS:
+// half 0 writes Z[k], half 1 Z[G/2 - k], both as (own + conj(other)) +
+// i (own - conj(other)) w with w = e^{2 pi i k / G}, resp.
+// e^{2 pi i (G/2 - k) / G} (one workgroup holding both rows' results in
+// registers needed 252 VGPRs, one workgroup per CU).
 template<int G>
-__global__ void __launch_bounds__(RowPlan<G>::P)
+__global__ void __launch_bounds__(2 * RowPlan<G>::P)
 k_rows_herm(float2* __restrict__ grid, int k0, int M,
-        const float2* __restrict__ W, const uint64_t* __restrict__ masks)
+        const float2* __restrict__ W, const uint32_t* __restrict__ occ)
 {
     using F = RowFft<G, 1>;
-    constexpr int EPT = F::EPT, NW = mask_words(G), NQ = G / 4 + 1;
+    constexpr int P = RowPlan<G>::P, EPT = F::EPT;
+    constexpr int NC = occ_classes(G), NQ = G / 4 + 1;
+    static_assert(EPT == 16 && P == G / 16 && P % 64 == 0,
+            "element r of thread p at column p + r P (k_row_occupancy)");
+    constexpr int kRowLds = G + G / 16;            // float2 per row buffer
     extern __shared__ float2 lds[];
-    const int p = threadIdx.x;
+    const int half = threadIdx.x / P;              // wave-uniform
+    const int p = threadIdx.x - half * P;
+    float2* my_lds = lds + half * kRowLds;
+    const float2* other_lds = lds + (1 - half) * kRowLds;
     const Buf gb(grid - k0, grid_bytes(G, k0));
     F f;
     f.init(p, W, G);
     const int per = (NQ + gridDim.x - 1) / gridDim.x;
     const int q_begin = blockIdx.x * per, q_end = min(NQ, q_begin + per);
-    // H row u from grid rows u and -u (element v and -v); tiles with no
-    // bucketed entry were not written by the scatter and read as zero.
-    auto load_h = [&](float2 (&v)[EPT], int u, int pq) {
+    for (int k = q_begin; k < q_end; ++k)
+    {
+        const int pq = opaque(p);
+        // H row u from grid rows u and -u (elements v and -v); tiles with
+        // no bucketed entry were not written by the scatter: read as zero.
+        const int u = half ? G / 2 - k : k;        // k = G/4: both the same
         const int ur = (G - u) & (G - 1);
-        uint64_t wa[NW], wb[NW];
-#pragma unroll
-        for (int w = 0; w < NW; ++w)
-        {
-            wa[w] = masks ? masks[(u >> 6) * NW + w] : ~0ull;
-            wb[w] = masks ? masks[(ur >> 6) * NW + w] : ~0ull;
-        }
+        const uint32_t oa_bits = occ ?
+                occ[(u >> 6) * NC + (pq >> 6)] : 0xFFFFFFFFu;
+        const uint32_t ob_bits = occ ?
+                occ[(ur >> 6) * NC + ((pq + 63) >> 6)] >> 16 : 0xFFFFFFFFu;
         const uint32_t ra = ((uint32_t)u * G + k0) * 8u;
         const uint32_t rb = ((uint32_t)ur * G + k0) * 8u;
+        float2 v[EPT];
         F::load_input(v, [&](int c) {
             const int ca = pq + c, cb = (G - ca) & (G - 1);
-            const int ta = ca >> 6, tb = cb >> 6;
-            const bool oa = (wa[NW > 1 ? ta >> 6 : 0] >> (ta & 63)) & 1ull;
-            const bool ob = (wb[NW > 1 ? tb >> 6 : 0] >> (tb & 63)) & 1ull;
+            const bool oa = (oa_bits >> (c / P)) & 1u;
+            const bool ob = (ob_bits >> (c / P)) & 1u;
             const float2 a = gb.load_if(oa, ra + (uint32_t)ca * 8u);
             const float2 b = gb.load_if(ob, rb + (uint32_t)cb * 8u);
             return make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
         });
-    };
-    for (int k = q_begin; k < q_end; ++k)
-    {
-        const int pq = opaque(p);
-        const int ub = G / 2 - k;              // == k for the quad k = G/4
-        float2 va[EPT], vb[EPT];
-        load_h(va, k, pq);
-        f.transform(va, pq, lds, RowIdx{});
-        if (ub != k)
-        {
-            load_h(vb, ub, pq);
-            f.transform(vb, pq, lds, RowIdx{});
-        }
-        else
-        {
-#pragma unroll
-            for (int i = 0; i < EPT; ++i) vb[i] = va[i];
-        }
+        f.transform(v, pq, my_lds, RowIdx{});
+        // Swap the two halves' results (same thread layout in both).
+        __syncthreads();
+        F::store_output(v, [&](int c, int, float2 x) {
+            my_lds[RowIdx::off(pq + c)] = x;
+        });
+        __syncthreads();
         // e^{2 pi i k / G} = conj(W[k]); e^{2 pi i (G/2 - k) / G} = -W[k].
         const float2 wt = W[k];
-        const float2 wk = make_float2(wt.x, -wt.y);
-        const float2 wb = make_float2(-wt.x, -wt.y);
-        float2 za[EPT];
-#pragma unroll
-        for (int i = 0; i < EPT; ++i)
-        {
-            const float2 a = va[i], b = vb[i];
+        const float2 w = half ? make_float2(-wt.x, -wt.y)
+                              : make_float2(wt.x, -wt.y);
+        F::store_output(v, [&](int c, int i, float2 a) {
+            const float2 b = other_lds[RowIdx::off(pq + c)];
             const float2 xe = make_float2(a.x + b.x, a.y - b.y);
-            const float2 xo = cmul(make_float2(a.x - b.x, a.y + b.y), wk);
-            za[i] = make_float2(xe.x - xo.y, xe.y + xo.x);
-            // Z[G/2 - k] from the same pair, roles swapped.
-            const float2 ye = make_float2(b.x + a.x, b.y - a.y);
-            const float2 yo = cmul(make_float2(b.x - a.x, b.y + a.y), wb);
-            vb[i] = make_float2(ye.x - yo.y, ye.y + yo.x);
-        }
-        const uint32_t vo = (uint32_t)pq * 8u;
-        const uint32_t va_row = (uint32_t)k * G * 8u + vo;
-        F::store_output(za, [&](int c, int, float2 x) {
-            gb.store_if((unsigned)(pq + c - k0) < (unsigned)M, x, va_row + c * 8u);
+            const float2 xo = cmul(make_float2(a.x - b.x, a.y + b.y), w);
+            v[i] = make_float2(xe.x - xo.y, xe.y + xo.x);
         });
-        if (k > 0 && ub != k)
-        {
-            const uint32_t vb_row = (uint32_t)ub * G * 8u + vo;
-            F::store_output(vb, [&](int c, int, float2 x) {
-                gb.store_if((unsigned)(pq + c - k0) < (unsigned)M, x,
-                        vb_row + c * 8u);
-            });
-        }
+        // Half 0: Z row k; half 1: Z row G/2 - k (not for k = 0, G/4).
+        const bool write = !half || (k > 0 && 2 * k < G / 2);
+        const uint32_t vr = (uint32_t)u * G * 8u + (uint32_t)pq * 8u;
+        F::store_output(v, [&](int c, int, float2 x) {
+            gb.store_if(write && (unsigned)(pq + c - k0) < (unsigned)M, x,
+                    vr + c * 8u);
+        });
     }
 }
 
@@ -1187,6 +1196,195 @@ k_rows_image(float2* __restrict__ grid, int k0, int M,
     }
 }
 
+// Degridding, 2-D: the real-input form -------------------------------------
+//
+// The corrected image is real, so its transform is Hermitian: A[-u][-v] =
+// conj(A[u][v]). The column passes transform the image row pairs
+// z[m] = f[2m] + i f[2m + 1] with a length-G/2 complex transform Z
+// (four-step over G/2 rows of the grid buffer), and the row pass recovers
+// the column spectra X[k] = (Z[k] + conj Z[G/2 - k]) / 2 - i (Z[k] -
+// conj Z[G/2 - k]) e^{-2 pi i k / G} / 2, k in [0, G/2], from quads (Z rows
+// k and G/2 - k, swapped between the two halves of the workgroup through
+// LDS), transforms them along the rows and writes each grid row u together
+// with row G - u, the conjugate of row u reversed. Traffic per call at
+// config 2: ~1.3 GB instead of ~2.1 GB.
+
+// Column pass A (forward) with the 2-D image prologue: for n1 = blockIdx.x,
+// length-N2 FFTs over m = n1 + N1 n2 of z[m] = f[2m] + i f[2m + 1] (image
+// rows 2m - k0 and 2m + 1 - k0, corrected in place, checkerboard), times
+// e^{-2 pi i n1 k2 / (G/2)}, into rows N2 n1 + k2 (row pitch G).
+template<int N1, int N2>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+k_cols_a_image_herm(float* __restrict__ dirty, float2* __restrict__ grid,
+        ImageParams<float> ip, int k0, int M, const float2* __restrict__ W)
+{
+#pragma clang fp contract(off)
+    constexpr int G = 2 * N1 * N2, B = ColPlan<N2>::B;
+    using F = ColFft<N2, -1>;
+    extern __shared__ float2 lds[];
+    const int c = threadIdx.x % B, p = threadIdx.x / B;
+    const int n1 = blockIdx.x;
+    const int h = M / 2;
+    const Buf gb(grid, grid_bytes(G, 0));
+    const BufF db(dirty, (uint32_t)((size_t)ip.N * ip.N * 4));
+    F f;
+    f.init(p, W, G);
+    float2 fs[F::EPT];
+#pragma unroll
+    for (int i = 0; i < F::EPT; ++i)
+        fs[i] = F::twiddle(W, 2 * n1 * F::out_index(p, i));
+    const int ncb = (M + B - 1) / B;
+    const uint32_t so = (uint32_t)N2 * n1 * G * 8u;
+    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
+    {
+        const int pq = opaque(p), cq = opaque(c);
+        const int col = cb * B + cq;
+        const bool ok = col < M;
+        float2 v[F::EPT];
+        const float ccx = ip.conv_corr[min(abs(col - h), h)];
+        // All image loads first, then the in-place correction stores (see
+        // k_cols_a_image).
+        static_assert(F::EPT == 16, "one input slot per element (R0 = 16)");
+        F::load_input(v, [&](int e) {
+            const int iy = 2 * (n1 + N1 * (pq + e)) - k0;
+            const bool in0 = ok && (unsigned)iy < (unsigned)M;
+            const bool in1 = ok && (unsigned)(iy + 1) < (unsigned)M;
+            return make_float2(
+                    db.load_if(in0, ((uint32_t)iy * ip.N + col) * 4u),
+                    db.load_if(in1, ((uint32_t)(iy + 1) * ip.N + col) * 4u));
+        });
+        F::load_input(v, [&](int e) {
+            const int iy0 = 2 * (n1 + N1 * (pq + e)) - k0;
+            const float2 x = v[e / (N2 / 16)];
+            float out[2];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+            {
+                const int iy = iy0 + j;
+                const bool in = ok && (unsigned)iy < (unsigned)M;
+                float val = j ? x.y : x.x;
+                // inv_correction (es_image_dev.h), 2-D branch.
+                const float ccy = ip.conv_corr[min(abs(iy - h), h)];
+                const float corr = ccx * ccy * ip.norm * ip.norm;
+                val *= 1.0f / corr;
+                db.store_if(in, val, ((uint32_t)iy * ip.N + col) * 4u);
+                if ((col + iy) & 1) val = -val;
+                out[j] = val;
+            }
+            return make_float2(out[0], out[1]);
+        });
+        f.transform(v, pq, lds, ColIdx<B>{cq});
+        const uint32_t vo = ((uint32_t)pq * G + col) * 8u;
+        F::store_output(v, [&](int e, int i, float2 x) {
+            if (ok) gb.store(cmul(x, fs[i]), vo, so + e * (uint32_t)G * 8u);
+        });
+    }
+}
+
+// Column pass B (forward) of the half-length transform: for k2 =
+// blockIdx.x, length-N1 FFTs over rows k2 + N2 n1, results back into rows
+// k2 + N2 k1 (natural order Z[k] in row k; row pitch G).
+template<int N1, int N2>
+__global__ void __launch_bounds__(256)
+k_cols_b_image_herm(float2* __restrict__ grid, int M,
+        const float2* __restrict__ W)
+{
+    constexpr int G = 2 * N1 * N2, B = ColPlan<N1>::B;
+    using F = ColFft<N1, -1>;
+    extern __shared__ float2 lds[];
+    const int c = threadIdx.x % B, p = threadIdx.x / B;
+    const int k2 = blockIdx.x;
+    const Buf gb(grid, grid_bytes(G, 0));
+    F f;
+    f.init(p, W, G);
+    const int ncb = (M + B - 1) / B;
+    const uint32_t so = (uint32_t)k2 * G * 8u;
+    constexpr uint32_t kStep = (uint32_t)N2 * G * 8u;
+    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
+    {
+        const int pq = opaque(p), cq = opaque(c);
+        const int col = cb * B + cq;
+        const bool ok = col < M;
+        const uint32_t vo = ((uint32_t)pq * N2 * G + col) * 8u;
+        float2 v[F::EPT];
+        F::load_input(v, [&](int e) {
+            return ok ? gb.load(vo, so + e * kStep) : make_float2(0.f, 0.f);
+        });
+        f.transform(v, pq, lds, ColIdx<B>{cq});
+        F::store_output(v, [&](int e, int, float2 x) {
+            if (ok) gb.store(x, vo, so + e * kStep);
+        });
+    }
+}
+
+// Row pass (forward) of the real-input form: quads as k_rows_herm; half 0
+// forms X[k] (grid rows k and G - k), half 1 X[G/2 - k] (rows G/2 - k and
+// G/2 + k; for k = 0 the row G/2 alone, for k = G/4 nothing). Only the
+// tiles the gather reads are written (k_row_occupancy<true>).
+template<int G>
+__global__ void __launch_bounds__(2 * RowPlan<G>::P)
+k_rows_image_herm(float2* __restrict__ grid, int k0, int M,
+        const float2* __restrict__ W, const uint32_t* __restrict__ need)
+{
+    using F = RowFft<G, -1>;
+    constexpr int P = RowPlan<G>::P, EPT = F::EPT;
+    constexpr int NC = occ_classes(G), NQ = G / 4 + 1;
+    static_assert(EPT == 16 && P == G / 16 && P % 64 == 0,
+            "element r of thread p at column p + r P (k_row_occupancy)");
+    constexpr int kRowLds = G + G / 16;
+    extern __shared__ float2 lds[];
+    const int half = threadIdx.x / P;
+    const int p = threadIdx.x - half * P;
+    float2* my_lds = lds + half * kRowLds;
+    const float2* other_lds = lds + (1 - half) * kRowLds;
+    const Buf gb(grid - k0, grid_bytes(G, k0));
+    F f;
+    f.init(p, W, G);
+    const int per = (NQ + gridDim.x - 1) / gridDim.x;
+    const int q_begin = blockIdx.x * per, q_end = min(NQ, q_begin + per);
+    for (int k = q_begin; k < q_end; ++k)
+    {
+        const int pq = opaque(p);
+        const int u = half ? G / 2 - k : k;         // X row (k = G/4: same)
+        const int zr = u & (G / 2 - 1);             // Z[G/2] = Z[0]
+        float2 v[EPT];
+        const uint32_t vz = (uint32_t)zr * G * 8u + (uint32_t)pq * 8u;
+        F::load_input(v, [&](int c) {
+            return gb.load_if((unsigned)(pq + c - k0) < (unsigned)M, vz + c * 8u);
+        });
+        // Swap the Z rows between the halves (input slot r = column p + r P).
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < EPT; ++r) my_lds[RowIdx::off(pq + r * P)] = v[r];
+        __syncthreads();
+        // e^{-2 pi i k / G} = W[k]; e^{-2 pi i (G/2 - k) / G} = -conj(W[k]).
+        const float2 wt = W[k];
+        const float2 w = half ? make_float2(-wt.x, wt.y) : wt;
+#pragma unroll
+        for (int r = 0; r < EPT; ++r)
+        {
+            const float2 a = v[r], b = other_lds[RowIdx::off(pq + r * P)];
+            const float2 dw = cmul(make_float2(a.x - b.x, a.y + b.y), w);
+            v[r] = make_float2(0.5f * ((a.x + b.x) + dw.y),
+                    0.5f * ((a.y - b.y) - dw.x));
+        }
+        f.transform(v, pq, my_lds, RowIdx{});
+        const bool write = !half || 2 * k != G / 2;
+        const int ur = (G - u) & (G - 1);
+        const uint32_t nf = need ? need[(u >> 6) * NC + (pq >> 6)] : ~0u;
+        const uint32_t nr = need ?
+                need[(ur >> 6) * NC + ((pq + 63) >> 6)] >> 16 : ~0u;
+        const uint32_t ro = ((uint32_t)u * G + k0) * 8u + (uint32_t)pq * 8u;
+        const uint32_t rr = ((uint32_t)ur * G + k0) * 8u;
+        F::store_output(v, [&](int c, int, float2 x) {
+            gb.store_if(write && ((nf >> (c / P)) & 1u), x, ro + c * 8u);
+            const int cr = (G - pq - c) & (G - 1);
+            gb.store_if(write && ur != u && ((nr >> (c / P)) & 1u),
+                    make_float2(x.x, -x.y), rr + (uint32_t)cr * 8u);
+        });
+    }
+}
+
 // Launch helpers --------------------------------------------------------------
 
 int num_cus()
@@ -1321,13 +1519,25 @@ bool herm_enabled(const ImageParams<float>& ip)
     return on && !ip.do_w && ip.G >= 2048 && ip.G <= 8192;
 }
 
+// The same for degridding (env SDP_ES_HERM_DEGRID=0: the complex form).
+bool herm_degrid_enabled(const ImageParams<float>& ip)
+{
+    static int on = -1;
+    if (on < 0)
+    {
+        const char* e = getenv("SDP_ES_HERM_DEGRID");
+        on = (e && e[0] == '0') ? 0 : 1;
+    }
+    return on && !ip.do_w && ip.G >= 2048 && ip.G <= 8192;
+}
+
 template<int N1, int N2>
 int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
-        const uint32_t* tiles, int ncoarse, uint64_t* masks,
+        const uint32_t* tiles, int ncoarse, uint32_t* occ,
         hipStream_t stream)
 {
     constexpr int G = N1 * N2;
-    if constexpr (G < 2048)
+    if constexpr (G < 2048 || G > 8192)
     {
         return SDP_ERR_INVALID_ARGUMENT;
     }
@@ -1337,17 +1547,20 @@ int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
         sdp_Error st = SDP_SUCCESS;
         if (tiles)
         {
-            if (!masks) return SDP_ERR_RUNTIME;
-            k_tile_masks<<<G / 64, 64, 0, stream>>>(tiles, ncoarse, G / 64,
-                    mask_words(G), masks);
+            if (!occ) return SDP_ERR_RUNTIME;
+            static_assert(32 * occ_classes(G) <= 320, "one bit per thread");
+            k_row_occupancy<false><<<G / 64, 320, 0, stream>>>(tiles,
+                    ncoarse, G, occ);
             SDP_HIP_CHECK_LAUNCH(&st);
             if (st) return st;
         }
-        const size_t lds = row_lds_bytes(G);
+        const size_t lds = 2 * row_lds_bytes(G);
         SDP_HIP_CHECK((allow_lds<k_rows_herm<G>>(lds)), &st);
         if (st) return st;
-        k_rows_herm<G><<<row_blocks(G), RowPlan<G>::P, lds, stream>>>(
-                grid, g.k0, g.M, W, tiles ? masks : nullptr);
+        const int blocks = std::min(G / 4 + 1, num_cus() *
+                (int)std::max<size_t>(1, (160 * 1024) / lds));
+        k_rows_herm<G><<<blocks, 2 * RowPlan<G>::P, lds, stream>>>(
+                grid, g.k0, g.M, W, tiles ? occ : nullptr);
         SDP_HIP_CHECK_LAUNCH(&st);
         if (st) return st;
         k_cols_a_herm<HS::N1, HS::N2><<<col_grid<k_cols_a_herm<HS::N1,
@@ -1363,7 +1576,7 @@ int grid_to_image_herm(const Geometry& g, const ImageParams<float>& ip,
         const float2* W, const float2* grid, float* dirty, hipStream_t stream)
 {
     constexpr int G = N1 * N2;
-    if constexpr (G < 2048)
+    if constexpr (G < 2048 || G > 8192)
     {
         return SDP_ERR_INVALID_ARGUMENT;
     }
@@ -1374,6 +1587,66 @@ int grid_to_image_herm(const Geometry& g, const ImageParams<float>& ip,
         k_cols_b_herm<HS::N1, HS::N2><<<col_grid<k_cols_b_herm<HS::N1,
                 HS::N2>>(HS::N2, g.M, ColPlan<HS::N1>::B), 256, kColLdsBytes,
                 stream>>>(grid, dirty, ip, g.k0, g.M, W);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        return st;
+    }
+}
+
+template<int N1, int N2>
+int image_cols_herm(const Geometry& g, const ImageParams<float>& ip,
+        const float2* W, float* dirty, float2* grid, hipStream_t stream)
+{
+    constexpr int G = N1 * N2;
+    if constexpr (G < 2048 || G > 8192)
+    {
+        return SDP_ERR_INVALID_ARGUMENT;
+    }
+    else
+    {
+        using HS = HalfSplit<G / 2>;
+        sdp_Error st = SDP_SUCCESS;
+        k_cols_a_image_herm<HS::N1, HS::N2><<<col_grid<k_cols_a_image_herm<
+                HS::N1, HS::N2>>(HS::N1, g.M, ColPlan<HS::N2>::B), 256,
+                kColLdsBytes, stream>>>(dirty, grid, ip, g.k0, g.M, W);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        return st;
+    }
+}
+
+template<int N1, int N2>
+int image_to_grid_herm(const Geometry& g, const float2* W, float2* grid,
+        const uint32_t* tiles, int ncoarse, uint32_t* need,
+        hipStream_t stream)
+{
+    constexpr int G = N1 * N2;
+    if constexpr (G < 2048 || G > 8192)
+    {
+        return SDP_ERR_INVALID_ARGUMENT;
+    }
+    else
+    {
+        using HS = HalfSplit<G / 2>;
+        sdp_Error st = SDP_SUCCESS;
+        if (tiles)
+        {
+            if (!need) return SDP_ERR_RUNTIME;
+            k_row_occupancy<true><<<G / 64, 320, 0, stream>>>(tiles,
+                    ncoarse, G, need);
+            SDP_HIP_CHECK_LAUNCH(&st);
+            if (st) return st;
+        }
+        k_cols_b_image_herm<HS::N1, HS::N2><<<col_grid<k_cols_b_image_herm<
+                HS::N1, HS::N2>>(HS::N2, g.M, ColPlan<HS::N1>::B), 256,
+                kColLdsBytes, stream>>>(grid, g.M, W);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        if (st) return st;
+        const size_t lds = 2 * row_lds_bytes(G);
+        SDP_HIP_CHECK((allow_lds<k_rows_image_herm<G>>(lds)), &st);
+        if (st) return st;
+        const int blocks = std::min(G / 4 + 1, num_cus() *
+                (int)std::max<size_t>(1, (160 * 1024) / lds));
+        k_rows_image_herm<G><<<blocks, 2 * RowPlan<G>::P, lds, stream>>>(
+                grid, g.k0, g.M, W, tiles ? need : nullptr);
         SDP_HIP_CHECK_LAUNCH(&st);
         return st;
     }
@@ -1504,7 +1777,7 @@ int fft_twiddles_create(int grid_size, FftTwiddles* tw)
             hipMemcpyHostToDevice), &st);
     if (!st && grid_size >= 2048)
         SDP_HIP_CHECK(hipMalloc(&tw->masks, (size_t)(grid_size / 64) *
-                mask_words(grid_size) * sizeof(uint64_t)), &st);
+                occ_classes(grid_size) * sizeof(uint32_t)), &st);
     tw->G = grid_size;
     return st;
 }
@@ -1525,7 +1798,7 @@ int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
     const float2* W = (const float2*)tw.table;
     if (herm_enabled(ip))
         SDP_ES_FFT_DISPATCH(g.G, (grid_rows_cols_herm<N1, N2>(g, W,
-                (float2*)grid, tiles, ncoarse, (uint64_t*)tw.masks, stream)))
+                (float2*)grid, tiles, ncoarse, (uint32_t*)tw.masks, stream)))
     SDP_ES_FFT_DISPATCH(g.G, (grid_rows_cols<N1, N2>(g, W, (float2*)grid,
             tiles, ncoarse, stream)))
 }
@@ -1548,6 +1821,9 @@ int fft_image_cols(const ImageParams<float>& ip, int plane,
 {
     const Geometry g = geometry(ip);
     const float2* W = (const float2*)tw.table;
+    if (herm_degrid_enabled(ip) && correct_in_place)
+        SDP_ES_FFT_DISPATCH(g.G, (image_cols_herm<N1, N2>(g, ip, W, dirty,
+                (float2*)grid, stream)))
     SDP_ES_FFT_DISPATCH(g.G, (image_cols<N1, N2>(g, ip, plane, W, dirty,
             correct_in_place, (float2*)grid, stream)))
 }
@@ -1557,6 +1833,9 @@ int fft_image_to_grid(const ImageParams<float>& ip, const FftTwiddles& tw,
 {
     const Geometry g = geometry(ip);
     const float2* W = (const float2*)tw.table;
+    if (herm_degrid_enabled(ip))
+        SDP_ES_FFT_DISPATCH(g.G, (image_to_grid_herm<N1, N2>(g, W,
+                (float2*)grid, tiles, ncoarse, (uint32_t*)tw.masks, stream)))
     SDP_ES_FFT_DISPATCH(g.G, (image_to_grid<N1, N2>(g, W, (float2*)grid,
             tiles, ncoarse, stream)))
 }
