@@ -9,6 +9,9 @@ screen / correction kernels by three fused passes. Checked here:
     benchmark geometry (G = 8192, N = 5440) and at G = 16384, where the
     float64 oracle FFT would take minutes -- relative L2 < 2e-6;
   * the split scatter/finish API and odd-N untouched last row/column.
+2-D plans with 2048 <= G <= 8192 take the real-output (gridding) and
+real-input (degridding) forms of the transform (half-length column passes);
+the cases above at G = 2048, 4096 and 8192 cover them, odd N included.
 """
 import os
 
@@ -65,6 +68,8 @@ ORACLE_CASES = [
     (840, False, 0.05),    # 1024, config-1 kernel (W = 4)
     (1360, False, 1e-5),   # 2048
     (1349, True, 1e-5),    # 2048, odd N, w-stacking
+    (1349, False, 1e-5),   # 2048, odd N, 2-D (real-output / real-input form)
+    (2701, False, 1e-5),   # 4096, odd N, 2-D
     (680, True, 1e-5),     # 1024, w-stacking
     (2720, False, 1e-5),   # 4096
 ]
