@@ -1,5 +1,10 @@
 #!/bin/bash
 # A/B of k_tower_idft variants: parity tests on one variant, bench on all.
+# The variants are library builds made beforehand with scripts/variant_lib.sh
+# (round 3: base = the HEAD source via REPLACES=..., c16w5 / c16w6 / c32w4 =
+# -DSDP_IDFT_CAP=16|32 -DTOWER_IDFT_WAVES=5|6|4), e.g.
+#   scripts/variant_lib.sh c16w6 csrc/grid_data/sdp_grid_wstack_wtower.hip \
+#       -DSDP_IDFT_CAP=16 -DTOWER_IDFT_WAVES=6
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/wt_ab; mkdir -p $OUT
 SKA_SDP_FUNC_LIB_DIR=variants/c16w5 timeout -k 10 300 python -u -m pytest tests/test_wstack_gpu.py tests/test_wtower_vla_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/tests.log 2>&1 || { tail -20 $OUT/tests.log; exit 1; }
