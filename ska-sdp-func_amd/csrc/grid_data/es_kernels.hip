@@ -857,90 +857,6 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
     }
 }
 
-// Persistent form of k_bucket_fill2: a workgroup walks the (super bin,
-// chunk group) items blockIdx.x, + gridDim.x, ... and issues the next
-// item's dependent prologue loads (its tiles' window starts and its record
-// range) before moving the current item's records, so their round trips
-// overlap the current stores instead of opening every item.
-#ifndef SDP_FILL2_PERSIST
-#define SDP_FILL2_PERSIST 0
-#endif
-template<typename T, int MODE, bool DO_W>
-__global__ __launch_bounds__(256) void k_bucket_fill2p(EsParams<T> p, int nc,
-        int gc, int ngroups, const uint32_t* __restrict__ table,
-        const uint32_t* __restrict__ bin_start,
-        const uint32_t* __restrict__ sb_start, const T* __restrict__ recs1,
-        T* __restrict__ recs)
-{
-    constexpr int kWords = Rec<T, MODE, DO_W>::kWords;
-    __shared__ uint32_t cur[kMaxSuperTiles];
-    const int t = threadIdx.x;
-    const int S = 1 << p.sshift;
-    const int nitems = ngroups * p.nsbins;
-    auto prologue = [&](int i, uint32_t& curv, uint32_t& e0, uint32_t& e1) {
-        const int sb = i / ngroups, g = i - sb * ngroups;
-        const int c0 = g * gc, c1 = min(nc, c0 + gc);
-        const int su = sb / p.nsuper, sv = sb - su * p.nsuper;
-        curv = 0u;
-        if (t < S * S)
-        {
-            const int tu = (su << p.sshift) + (t >> p.sshift);
-            const int tv = (sv << p.sshift) + (t & (S - 1));
-            if (tu < p.ntiles && tv < p.ntiles)
-            {
-                const int f = fine_bin(p, tu, tv);
-                curv = bin_start[f] + table[(size_t)c0 * p.tstride + f];
-            }
-        }
-        const uint32_t* col = table + p.nbins + sb;
-        e0 = sb_start[sb] + col[(size_t)c0 * p.tstride];
-        e1 = c1 < nc ? sb_start[sb] + col[(size_t)c1 * p.tstride] :
-                sb_start[sb + 1];
-    };
-    int i = blockIdx.x;
-    if (i >= nitems) return;
-    uint32_t curv, e0, e1;
-    prologue(i, curv, e0, e1);
-    for (; i < nitems; i += gridDim.x)
-    {
-        __syncthreads();   // the previous item's cursor atomics are done
-        if (t < S * S) cur[t] = curv;
-        __syncthreads();
-        const uint32_t ce0 = e0, ce1 = e1;
-        const int sb = i / ngroups;
-        const int su = sb / p.nsuper, sv = sb - su * p.nsuper;
-        const int tu_base = su << p.sshift, tv_base = sv << p.sshift;
-        if (i + (int)gridDim.x < nitems)
-            prologue(i + (int)gridDim.x, curv, e0, e1);
-        constexpr int kIn = 4;
-        for (uint32_t e = ce0 + t; e < ce1; e += 256 * kIn)
-        {
-            T rec[kIn][kWords];
-#pragma unroll
-            for (int q = 0; q < kIn; ++q)
-                if (e + q * 256 < ce1)
-                    copy_rec<T, kWords>(rec[q], recs1 + (size_t)(e + q * 256) * kWords);
-#pragma unroll
-            for (int q = 0; q < kIn; ++q)
-            {
-                if (e + q * 256 >= ce1) break;
-                int u0, u1, v0, v1, tu0, tu1, tv0, tv1;
-                tap_range(p, rec[q][0], rec[q][1], u0, u1, v0, v1);
-                tile_span<T, MODE>(p, u0, u1, v0, v1, tu0, tu1, tv0, tv1);
-                tu0 = max(tu0, tu_base); tu1 = min(tu1, tu_base + S - 1);
-                tv0 = max(tv0, tv_base); tv1 = min(tv1, tv_base + S - 1);
-                for (int tu = tu0; tu <= tu1; ++tu)
-                    for (int tv = tv0; tv <= tv1; ++tv)
-                    {
-                        const int j = ((tu - tu_base) << p.sshift) | (tv - tv_base);
-                        const uint32_t pos = atomicAdd(&cur[j], 1u);
-                        store_rec<T, kWords>(recs + (size_t)pos * kWords, rec[q]);
-                    }
-            }
-        }
-    }
-}
-
 // Zero the grid cells of tiles that several work items share.
 template<typename T>
 __global__ __launch_bounds__(kThreads) void k_zero_shared_tiles(
@@ -2171,30 +2087,9 @@ void launch_fill(int nc, int64_t chunk, const EsParams<T>& p,
     const int groups = std::min(nc, SDP_FILL2_GROUPS);
     const int gc = (nc + groups - 1) / groups;
     const int ng = (nc + gc - 1) / gc;
-    // (one prologue cursor per thread: super bins of at most 256 tiles)
-    if (SDP_FILL2_PERSIST && (1 << (2 * p.sshift)) <= 256)
-    {
-        static int cus = 0;
-        if (!cus)
-        {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                    hipDeviceGetAttribute(&cus,
-                            hipDeviceAttributeMultiprocessorCount, dev) !=
-                    hipSuccess || cus <= 0)
-                cus = 256;
-        }
-        const int items = ng * p.nsbins;
-        k_bucket_fill2p<T, MODE, DO_W><<<std::min(items, cus * 8), 256, 0,
-                stream>>>(p, nc, gc, ng, s->table, s->bin_start, s->sb_start,
-                (const T*)s->recs1, (T*)s->recs);
-    }
-    else
-    {
-        k_bucket_fill2<T, MODE, DO_W><<<dim3(ng, p.nsbins), 256, 0,
-                stream>>>(p, nc, gc, s->table, s->bin_count, s->bin_start,
-                s->sb_start, (const T*)s->recs1, (T*)s->recs);
-    }
+    k_bucket_fill2<T, MODE, DO_W><<<dim3(ng, p.nsbins), 256, 0, stream>>>(
+            p, nc, gc, s->table, s->bin_count, s->bin_start, s->sb_start,
+            (const T*)s->recs1, (T*)s->recs);
 }
 
 #define SDP_ES_BY_THREADS(NTV, CALL) \
