@@ -1,8 +1,8 @@
 /* MI355X-native gridder utilities of the w-towers path: drop-in C ABI.
  *
- * The subset of src/ska-sdp-func/grid_data/sdp_gridder_utils.h and
- * sdp_gridder_clamp_channels.h (ska-sdp-func 1.2.2) that the w-towers
- * gridder and its tests use; same names, arguments and semantics.
+ * src/ska-sdp-func/grid_data/sdp_gridder_utils.h of ska-sdp-func 1.2.2
+ * (the channel clamps are in sdp_gridder_clamp_channels.h, as in the
+ * reference); same names, arguments and semantics.
  * Table generators (make_kernel, make_pswf_kernel, make_w_pattern) fill
  * host (CPU) arrays, as in the reference; the array operations run on the
  * GPU for device arrays and stage host arrays through device memory.
@@ -10,6 +10,7 @@
 #ifndef SDP_GRIDDER_UTILS_H_
 #define SDP_GRIDDER_UTILS_H_
 
+#include "ska-sdp-func/math/sdp_math_macros.h"
 #include "ska-sdp-func/utility/sdp_mem.h"
 
 #ifdef __cplusplus
@@ -122,42 +123,6 @@ void sdp_gridder_uvw_bounds_all(
         const sdp_Mem* end_chs,
         double uvw_min[3],
         double uvw_max[3],
-        sdp_Error* status
-);
-
-/* Channel ranges restricted to min_u <= u < max_u in dimension dim,
- * sdp_gridder_clamp_channels.h:42-56 (impl clamp_channels.cpp). */
-void sdp_gridder_clamp_channels_single(
-        const sdp_Mem* uvws,
-        const int dim,
-        const double freq0_hz,
-        const double dfreq_hz,
-        const sdp_Mem* start_ch_in,
-        const sdp_Mem* end_ch_in,
-        const double min_u,
-        const double max_u,
-        sdp_Mem* start_ch_out,
-        sdp_Mem* end_ch_out,
-        int64_t start_row,
-        int64_t end_row,
-        sdp_Error* status
-);
-
-/* Same in u and v, sdp_gridder_clamp_channels.h:72-87. */
-void sdp_gridder_clamp_channels_uv(
-        const sdp_Mem* uvws,
-        const double freq0_hz,
-        const double dfreq_hz,
-        const sdp_Mem* start_ch_in,
-        const sdp_Mem* end_ch_in,
-        const double min_u,
-        const double max_u,
-        const double min_v,
-        const double max_v,
-        sdp_Mem* start_ch_out,
-        sdp_Mem* end_ch_out,
-        int64_t start_row,
-        int64_t end_row,
         sdp_Error* status
 );
 

@@ -12,6 +12,7 @@
 // out-of-place plans are created on first use and cached in the handle
 // (exec_shift always runs in place). Host arrays are staged through HBM:
 // the transform itself always runs on the GPU (there is no CPU FFT here).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -181,11 +182,15 @@ template<typename T>
 __global__ void k_fft_phase(T* data, int64_t nx, int64_t ny)
 {
     const int64_t iy = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    const int64_t ix = blockIdx.y;
-    if (iy >= ny || ((ix + iy) & 1) == 0) return;
-    T* p = data + 2 * (ix * ny + iy);
-    p[0] = -p[0];
-    p[1] = -p[1];
+    if (iy >= ny) return;
+    // Rows stride over the y-grid (capped at 65535 blocks by the host).
+    for (int64_t ix = blockIdx.y; ix < nx; ix += gridDim.y)
+    {
+        if (((ix + iy) & 1) == 0) continue;
+        T* p = data + 2 * (ix * ny + iy);
+        p[0] = -p[0];
+        p[1] = -p[1];
+    }
 }
 
 // data *= factor (sdp_fft.cu:21-29), factor in double converted to T as
@@ -410,15 +415,11 @@ void sdp_fft_phase(sdp_Mem* data, sdp_Error* status)
     if (!have_gpu(status)) return;
     const int64_t nx = (nd == 2) ? sdp_mem_shape_dim(data, 0) : 1;
     const int64_t ny = sdp_mem_shape_dim(data, nd - 1);
-    if (nx > 65535 * 32768LL)
-    {
-        *status = SDP_ERR_INVALID_ARGUMENT;
-        return;
-    }
     DevArray d;
     d.init(data, status);
     if (*status) return;
-    const dim3 blocks(sdp_hip::blocks_for(ny, 256), (unsigned)nx);
+    const dim3 blocks(sdp_hip::blocks_for(ny, 256),
+            (unsigned)std::min<int64_t>(nx, 65535));
     if (t == SDP_MEM_COMPLEX_FLOAT)
         k_fft_phase<float><<<blocks, 256>>>((float*)sdp_mem_data(d.mem), nx,
                 ny);

@@ -68,16 +68,23 @@ int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
 int fft_grid_to_image(const ImageParams<float>& ip, int plane,
         const FftTwiddles& tw, float* grid, float* dirty, hipStream_t stream);
 
+// Degridding: whether the two halves below run in the real-input form
+// (half-length column transforms of the real image; 2-D, 2048 <= G <=
+// 8192, the image corrected in place). Decided ONCE per call by the caller
+// and passed to both halves, whose layouts must agree.
+bool fft_degrid_real_form(const ImageParams<float>& ip,
+        bool correct_in_place);
 // Degridding, part 1: image prologue (2-D: correct dirty in place) + first
 // column pass into the grid buffer.
 int fft_image_cols(const ImageParams<float>& ip, int plane,
         const FftTwiddles& tw, float* dirty, bool correct_in_place,
-        float* grid, hipStream_t stream);
+        bool real_form, float* grid, hipStream_t stream);
 // Degridding, part 2: second column pass + row pass writing the grid:
 // every cell (tiles == nullptr), or only the tiles the gather of this
 // bucketing reads (tiles = BucketScratch::bin_count of the degrid bins).
 int fft_image_to_grid(const ImageParams<float>& ip, const FftTwiddles& tw,
-        float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream);
+        float* grid, const uint32_t* tiles, int ncoarse, bool real_form,
+        hipStream_t stream);
 
 // Whole-grid 2-D FFT of a complex-float G x G grid in place, unnormalised
 // (forward e^-, inverse e^+, as rocFFT / cuFFT), in three passes (rows,

@@ -1821,13 +1821,23 @@ int fft_grid_to_image(const ImageParams<float>& ip, int plane,
             (const float2*)grid, dirty, stream)))
 }
 
+bool fft_degrid_real_form(const ImageParams<float>& ip,
+        bool correct_in_place)
+{
+    return herm_degrid_enabled(ip) && correct_in_place;
+}
+
 int fft_image_cols(const ImageParams<float>& ip, int plane,
         const FftTwiddles& tw, float* dirty, bool correct_in_place,
-        float* grid, hipStream_t stream)
+        bool real_form, float* grid, hipStream_t stream)
 {
     const Geometry g = geometry(ip);
     const float2* W = (const float2*)tw.table;
-    if (herm_degrid_enabled(ip) && correct_in_place)
+    // The real-input form corrects the image in place in its prologue and
+    // exists for the 2-D grids herm_degrid_enabled accepts only.
+    if (real_form && !fft_degrid_real_form(ip, correct_in_place))
+        return SDP_ERR_INVALID_ARGUMENT;
+    if (real_form)
         SDP_ES_FFT_DISPATCH(g.G, (image_cols_herm<N1, N2>(g, ip, W, dirty,
                 (float2*)grid, stream)))
     SDP_ES_FFT_DISPATCH(g.G, (image_cols<N1, N2>(g, ip, plane, W, dirty,
@@ -1835,11 +1845,13 @@ int fft_image_cols(const ImageParams<float>& ip, int plane,
 }
 
 int fft_image_to_grid(const ImageParams<float>& ip, const FftTwiddles& tw,
-        float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream)
+        float* grid, const uint32_t* tiles, int ncoarse, bool real_form,
+        hipStream_t stream)
 {
     const Geometry g = geometry(ip);
     const float2* W = (const float2*)tw.table;
-    if (herm_degrid_enabled(ip))
+    if (real_form && !herm_degrid_enabled(ip)) return SDP_ERR_INVALID_ARGUMENT;
+    if (real_form)
         SDP_ES_FFT_DISPATCH(g.G, (image_to_grid_herm<N1, N2>(g, W,
                 (float2*)grid, tiles, ncoarse, (uint32_t*)tw.masks, stream)))
     SDP_ES_FFT_DISPATCH(g.G, (image_to_grid<N1, N2>(g, W, (float2*)grid,

@@ -186,6 +186,34 @@ const int* int_ptr(const Staged& s)
     return s.dev ? (const int*)sdp_mem_data(s.dev) : nullptr;
 }
 
+// Shapes the DFT kernels index without bounds checks: lmn [n >= min_dirs,
+// 3] of the direction type, channel ranges int32 with one entry per uvw row
+// (checked when both are given). Returns false (status set) otherwise.
+bool check_dft_shapes(const sdp_Mem* uvws, const sdp_Mem* start_chs,
+        const sdp_Mem* end_chs, const sdp_Mem* lmn, int64_t min_dirs,
+        sdp_Error* status)
+{
+    const int64_t rows = sdp_mem_shape_dim(uvws, 0);
+    bool ok = sdp_mem_num_dims(lmn) == 2 && sdp_mem_shape_dim(lmn, 1) == 3 &&
+            sdp_mem_shape_dim(lmn, 0) >= min_dirs;
+    // As the reference, the ranges are used only when both are given.
+    const bool ranges = start_chs && end_chs;
+    for (const sdp_Mem* c : {start_chs, end_chs})
+    {
+        if (!ranges) break;
+        if (sdp_mem_type(c) != SDP_MEM_INT || sdp_mem_num_elements(c) < rows ||
+                !sdp_mem_is_c_contiguous(c))
+            ok = false;
+    }
+    if (!ok)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("lmn must be [n, 3]; start_chs / end_chs int32 arrays "
+                "with one entry per uvw row");
+    }
+    return ok;
+}
+
 // Subgrid offsets scaled as sdp_gridder_utils.cpp:171-178.
 void offsets(int ou, int ov, int ow, double theta, double w_step,
         double* du, double* dv, double* dw)
@@ -224,6 +252,19 @@ void image_to_flmn_t(const IMG* image, int size_l, int size_m, double theta,
             ++k;
         }
     }
+}
+
+// Non-zero pixels over the whole size_l x size_m region the fill loop of
+// image_to_flmn_t visits (the exported count follows the reference and
+// sees only shape[0] columns, so it cannot size the outputs of a
+// non-square image).
+template<typename IMG>
+int64_t count_nonzero_host(const IMG* image, int size_l, int size_m)
+{
+    int64_t k = 0;
+    for (int64_t i = 0; i < (int64_t)size_l * size_m; ++i)
+        k += image[i] != IMG(0);
+    return k;
 }
 
 } // namespace
@@ -310,6 +351,9 @@ void sdp_gridder_dft(const sdp_Mem* uvws, const sdp_Mem* start_chs,
         SDP_LOG_ERROR("Inconsistent array shapes");
         return;
     }
+    if (!check_dft_shapes(uvws, start_chs, end_chs, lmn,
+            sdp_mem_shape_dim(flux, 0), status))
+        return;
     if (!need_gpu(status)) return;
     Staged u, s, e, f, d, v;
     u.init(uvws, status);
@@ -375,6 +419,8 @@ void sdp_gridder_idft(const sdp_Mem* uvws, const sdp_Mem* vis,
     }
     const int64_t size = sdp_mem_shape_dim(image, 0);
     if (sdp_mem_num_dims(image) != 2 || sdp_mem_shape_dim(image, 1) != size ||
+            sdp_mem_num_dims(vis) != 2 || sdp_mem_num_dims(uvws) != 2 ||
+            sdp_mem_shape_dim(uvws, 1) != 3 ||
             sdp_mem_shape_dim(lmn, 0) < size * size ||
             sdp_mem_shape_dim(uvws, 0) != sdp_mem_shape_dim(vis, 0) ||
             (image_taper_1d &&
@@ -387,6 +433,8 @@ void sdp_gridder_idft(const sdp_Mem* uvws, const sdp_Mem* vis,
         SDP_LOG_ERROR("Inconsistent array shapes");
         return;
     }
+    if (!check_dft_shapes(uvws, start_chs, end_chs, lmn, size * size, status))
+        return;
     if (!need_gpu(status)) return;
     Staged u, vv, s, e, d, tp, im;
     u.init(uvws, status);
@@ -476,17 +524,37 @@ void sdp_gridder_image_to_flmn(const sdp_Mem* image, double theta,
         {
             img = sdp_mem_data_const(image);
         }
-        needed = sdp_gridder_count_nonzero_pixels(image, status);
-        if (*status)
+        if (sdp_mem_num_dims(image) != 2 || !sdp_mem_is_c_contiguous(image))
         {
+            *status = SDP_ERR_INVALID_ARGUMENT;
+            SDP_LOG_ERROR("Image must be a 2-D C-contiguous array");
             sdp_mem_free(host_img);
             return;
         }
+        if (img_t == SDP_MEM_DOUBLE)
+            needed = count_nonzero_host((const double*)img, size_l, size_m);
+        else if (img_t == SDP_MEM_FLOAT)
+            needed = count_nonzero_host((const float*)img, size_l, size_m);
+        else if (img_t == SDP_MEM_COMPLEX_DOUBLE)
+            needed = count_nonzero_host((const std::complex<double>*)img,
+                    size_l, size_m);
+        else
+            needed = count_nonzero_host((const std::complex<float>*)img,
+                    size_l, size_m);
         if (sdp_mem_shape_dim(flux, 0) < needed)
         {
             *status = SDP_ERR_INVALID_ARGUMENT;
             SDP_LOG_ERROR("flux array too small");
         }
+    }
+    if (!*status && image_taper_1d &&
+            (sdp_mem_type(image_taper_1d) != SDP_MEM_DOUBLE ||
+             sdp_mem_num_elements(image_taper_1d) <
+                     (int64_t)std::max(size_l, size_m)))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("image_taper_1d must be a double array of at least "
+                "max(image dims) entries");
     }
     if (!*status && (sdp_mem_num_dims(lmn) != 2 ||
             sdp_mem_shape_dim(lmn, 0) < needed ||

@@ -8,6 +8,7 @@
 // series of pswf_n at |2 w_step n|, the product inverted in double and
 // applied in the facet's precision; the w-stacking phasor from a reduced
 // phase). Host facets are staged through device memory.
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -27,20 +28,23 @@ __global__ void k_correct(AnyView facet, int nl, int nm, int off_l,
         int off_m, CorrParams cp, int mode)
 {
     const int im = blockIdx.x * blockDim.x + threadIdx.x;
-    const int il = blockIdx.y;
-    if (im >= nm || il >= nl) return;
-    const int pl = il - nl / 2 + off_l, pm = im - nm / 2 + off_m;
-    const int64_t i = (int64_t)il * nm + im;
-    if (mode == 0)
+    if (im >= nm) return;
+    // Rows stride over the y-grid (capped at 65535 blocks by the host).
+    for (int il = blockIdx.y; il < nl; il += gridDim.y)
     {
-        if (!corr_inside(pl, pm, cp)) return;
-        facet.store(i, correct_scaled(facet.load(i), facet.kind, pl, pm, cp,
-                pixel_scale(pl, pm, cp)));
-    }
-    else
-    {
-        facet.store(i, correct_scaled(facet.load(i), facet.kind, pl, pm, cp,
-                1.0));
+        const int pl = il - nl / 2 + off_l, pm = im - nm / 2 + off_m;
+        const int64_t i = (int64_t)il * nm + im;
+        if (mode == 0)
+        {
+            if (!corr_inside(pl, pm, cp)) continue;
+            facet.store(i, correct_scaled(facet.load(i), facet.kind, pl, pm,
+                    cp, pixel_scale(pl, pm, cp)));
+        }
+        else
+        {
+            facet.store(i, correct_scaled(facet.load(i), facet.kind, pl, pm,
+                    cp, 1.0));
+        }
     }
 }
 
@@ -105,7 +109,8 @@ void launch(sdp_Mem* facet, int off_l, int off_m, const CorrParams& cp,
     const int nm = (int)sdp_mem_shape_dim(facet, 1);
     if (nl <= 0 || nm <= 0) return;
     const AnyView v = {sdp_mem_data(f.dev), any_kind(sdp_mem_type(facet))};
-    k_correct<<<dim3((nm + 255) / 256, nl), 256>>>(v, nl, nm, off_l, off_m,
+    k_correct<<<dim3((nm + 255) / 256, std::min(nl, 65535)), 256>>>(v, nl,
+            nm, off_l, off_m,
             cp, mode);
     SDP_HIP_CHECK_LAUNCH(status);
     f.write_back(status);

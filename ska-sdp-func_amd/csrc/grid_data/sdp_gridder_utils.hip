@@ -11,6 +11,7 @@
 #include <cstring>
 #include <vector>
 
+#include "ska-sdp-func/grid_data/sdp_gridder_clamp_channels.h"
 #include "ska-sdp-func/grid_data/sdp_gridder_utils.h"
 #include "wtower_math.h"
 #include "wtower_ops.h"

@@ -370,13 +370,16 @@ void image_to_grid(sdp_GridderUvwEsFft* plan,
     {
         if (plan->fused_fft)
         {
+            const bool in_place = !plan->do_wstacking;
+            const bool real_form = sdp_es::fft_degrid_real_form(ip, in_place);
             e = sdp_es::fft_image_cols(ip, plane, plan->fft_tw, dirty,
-                    !plan->do_wstacking, grid, plan->stream);
+                    in_place, real_form, grid, plan->stream);
             if (e) { *status = (sdp_Error)e; return; }
             timing_mark(plan, 2);
             // Only the tiles this plane's gather reads are written.
             e = sdp_es::fft_image_to_grid(ip, plan->fft_tw, grid,
-                    plan->scratch.bin_count, plan->ncoarse, plan->stream);
+                    plan->scratch.bin_count, plan->ncoarse, real_form,
+                    plan->stream);
             if (e) *status = (sdp_Error)e;
             return;
         }

@@ -32,9 +32,104 @@ def _declared_functions():
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         text = re.sub(r"//[^\n]*", "", text)
         text = re.sub(r"#define[^\n]*(\\\n[^\n]*)*", "", text)
+        # Header-only (SDP_INLINE) functions are not library exports.
+        inline = set(re.findall(r"SDP_INLINE\s+\w+\s+(sdp_[a-z0-9_]+)\s*\(",
+                                text))
         for m in re.finditer(r"\b(sdp_[a-z0-9_]+)\s*\(", text):
-            names.add(m.group(1))
+            if m.group(1) not in inline:
+                names.add(m.group(1))
     return names
+
+
+# Every header path of the reference (ska-sdp-func 1.2.2, src/ska-sdp-func/)
+# that a C / C++ caller of the hot path and its SURVEY 8 rows includes.
+REFERENCE_HEADER_PATHS = [
+    "utility/sdp_mem.h", "utility/sdp_errors.h", "utility/sdp_logging.h",
+    "math/sdp_math_macros.h",
+    "fourier_transforms/sdp_fft.h", "fourier_transforms/sdp_fft_padded_size.h",
+    "fourier_transforms/sdp_pswf.h",
+    "grid_data/sdp_gridder_uvw_es_fft.h", "grid_data/sdp_gridder_wtower_uvw.h",
+    "grid_data/sdp_grid_wstack_wtower.h", "grid_data/sdp_gridder_utils.h",
+    "grid_data/sdp_gridder_clamp_channels.h",
+    "grid_data/sdp_gridder_wtower_height.h",
+    "grid_data/sdp_gridder_grid_correct.h",
+    "grid_data/sdp_degrid_uvw_custom.h",
+    "visibility/sdp_flagger.h", "visibility/sdp_weighting.h",
+    "visibility/sdp_tiled_functions.h", "visibility/sdp_opt_weighting.h",
+    "visibility/sdp_dft.h",
+    "clean/sdp_hogbom_clean.h", "clean/sdp_ms_clean_cornwell.h",
+]
+
+
+def test_reference_header_paths_exist():
+    missing = [h for h in REFERENCE_HEADER_PATHS if not os.path.exists(
+        os.path.join(ROOT, "include", "ska-sdp-func", h))]
+    assert not missing, f"reference header paths missing: {missing}"
+
+
+@pytest.mark.parametrize("lang", ["c", "c++"])
+def test_headers_compile_like_a_caller(tmp_path, lang):
+    """Every header, included by its reference path, compiles for a C (C99)
+    and a C++ (C++11) caller, all together in one translation unit."""
+    hdrs = sorted(os.path.relpath(h, os.path.join(ROOT, "include"))
+                  for h in glob.glob(os.path.join(ROOT, "include", "**",
+                                                  "*.h"), recursive=True))
+    src = tmp_path / ("all.c" if lang == "c" else "all.cpp")
+    src.write_text("".join(f'#include "{h}"\n' for h in hdrs)
+                   + "int main(void) { return 0; }\n")
+    cc, std = ("gcc", "-std=c99") if lang == "c" else ("g++", "-std=c++11")
+    r = subprocess.run([cc, std, "-Wall", "-Werror", "-fsyntax-only",
+                        "-I", os.path.join(ROOT, "include"), str(src)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
+def test_clamp_channels_inline_matches_oracle(tmp_path):
+    """The header-only sdp_gridder_clamp_channels_inline, compiled as C,
+    against the oracle's restatement of the reference inline
+    (sdp_gridder_clamp_channels.h:116-172) on random and edge cases."""
+    from oracle import wtower_oracle as wo
+
+    rng = np.random.default_rng(3)
+    cases = []
+    for _ in range(3000):
+        u = float(rng.choice([0.0, 1e-9, -1e-9]) if rng.random() < 0.1
+                  else rng.normal(0, 3000))
+        f0 = float(rng.uniform(1e8, 2e9))
+        df = float(rng.choice([0.0, 1e3]) if rng.random() < 0.1
+                   else rng.uniform(-5e6, 5e6))
+        s0, e0 = int(rng.integers(0, 50)), int(rng.integers(0, 400))
+        lo = float(rng.normal(0, 5000))
+        hi = lo + float(rng.choice([0.0, rng.uniform(0, 8000)]))
+        cases.append((u, f0, df, s0, e0, lo, hi))
+    inp = tmp_path / "in.txt"
+    inp.write_text("".join("%r %r %r %d %d %r %r\n" % c for c in cases))
+    src = tmp_path / "clamp.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stdint.h>\n'
+        '#include "ska-sdp-func/grid_data/sdp_gridder_clamp_channels.h"\n'
+        'int main(int argc, char** argv) {\n'
+        '  FILE* f = fopen(argv[1], "r"); double u, f0, df, lo, hi;\n'
+        '  long long s, e;\n'
+        '  while (fscanf(f, "%lf %lf %lf %lld %lld %lf %lf", &u, &f0, &df,'
+        ' &s, &e, &lo, &hi) == 7) {\n'
+        '    int64_t a = s, b = e;\n'
+        '    sdp_gridder_clamp_channels_inline(u, f0, df, &a, &b, lo, hi);\n'
+        '    printf("%lld %lld\\n", (long long)a, (long long)b); }\n'
+        '  return 0; }\n')
+    exe = tmp_path / "clamp"
+    subprocess.run(["gcc", "-std=c99", "-O2", "-I",
+                    os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+                    "-lm"], check=True)
+    out = subprocess.check_output([str(exe), str(inp)], text=True).split()
+    got = np.array(out, dtype=np.int64).reshape(-1, 2)
+    nonempty = 0
+    for (u, f0, df, s0, e0, lo, hi), (a, b) in zip(cases, got):
+        ref = wo.clamp_channels(u, f0, df, s0, e0, lo, hi)
+        assert (a, b) == tuple(int(x) for x in ref), (u, f0, df, s0, e0, lo,
+                                                     hi)
+        nonempty += b > a
+    assert nonempty > 150
 
 
 def test_library_exports_every_declared_symbol():

@@ -82,6 +82,25 @@ def test_pswf_plan_api():
     assert abs(Pswf(2, 5.0).evaluate(0.0) - 3.0) < 1e-12
 
 
+@pytest.mark.parametrize("m", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("c", [1.0, 2.5, 5.0, 8.0, 12.0, 20.0])
+def test_pswf_matches_specfun_all_orders(m, c):
+    """S_mm(c, x) for m >= 2 and x != 0 as well: scipy.special.pro_ang1 is
+    Zhang & Jin's specfun (SDMN / SCKB / ASWFA), the routines the reference
+    sdp_pswf.cpp:27-564 restates, so it stands in for the reference at every
+    order; agreement 1e-14 relative (c <= 12) and 1e-11 at c = 20, where
+    specfun's own power series loses digits."""
+    import scipy.special as sp
+    from ska_sdp_func.fourier_transforms import Pswf
+
+    p = Pswf(m, c)
+    xs = np.linspace(-0.98, 0.98, 41)
+    got = np.array([p.evaluate(x) for x in xs])
+    ref = np.array([sp.pro_ang1(m, m, c, abs(x))[0] for x in xs])
+    tol = 1e-14 if c <= 12 else 1e-11
+    assert np.max(np.abs(got - ref)) <= tol * np.max(np.abs(ref))
+
+
 def _padded_size_heap(n, padding_factor):
     """Restatement of sdp_fft_padded_size.cpp:87-126 (min-heap walk)."""
     heap = [2]

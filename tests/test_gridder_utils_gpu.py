@@ -183,6 +183,32 @@ def test_image_to_flmn_and_count(device, dtype, dir_t):
     np.testing.assert_array_equal(lmn_all, ra.astype(dir_t))
 
 
+def test_image_to_flmn_wide_image(device):
+    """A non-square image whose last columns (>= shape[0]) hold non-zero
+    pixels: outputs are sized by the pixels the fill visits, an undersized
+    flux array or a short taper is an argument error, not an overflow."""
+    import ska_sdp_func.grid_data as g
+    from ska_sdp_func.utility import CError
+
+    img = np.zeros((16, 40))
+    img[3, 5] = 1.0
+    img[7, 20] = 2.0
+    img[15, 39] = 3.0
+    img[0, 16] = 0.5
+    taper = np.linspace(0.5, 1.0, 40)
+    flux = np.zeros(4)
+    lmn = np.zeros((4, 3))
+    g.image_to_flmn(img, 0.02, 0.0, 0.0, taper, flux, lmn)
+    rf, rl = wo.image_to_flmn(img, 0.02, 0.0, 0.0, taper)
+    np.testing.assert_array_equal(flux, rf)
+    np.testing.assert_array_equal(lmn, rl)
+    with pytest.raises(CError, match="Error 2"):
+        g.image_to_flmn(img, 0.02, 0.0, 0.0, taper, np.zeros(3),
+                        np.zeros((3, 3)))
+    with pytest.raises(CError, match="Error 2"):
+        g.image_to_flmn(img, 0.02, 0.0, 0.0, taper[:16], flux, lmn)
+
+
 @pytest.mark.parametrize("ta,tb", [(np.complex128, np.complex128),
                                    (np.complex64, np.complex64),
                                    (np.complex128, np.complex64),
