@@ -59,6 +59,16 @@ void sdp_fft_norm(sdp_Mem* data, sdp_Error* status);
  * complex array, .h:128. */
 void sdp_fft_phase(sdp_Mem* data, sdp_Error* status);
 
+/* ---- MI355X extension (not in the reference ABI) ----------------------
+ * The w-stack plane transform of the w-towers gridder: a G x G complex-float
+ * GPU array, G a power of two in [1024, 16384], transformed in place
+ * (unnormalised; forward e^-, inverse e^+) by the fused three-pass FFT.
+ * The output's row k is STORED at row N1 (k mod N2) + k / N2 (G = N1 N2,
+ * N2 = sdp_fft_permuted_n2(G)); columns are in natural order. */
+void sdp_fft_2d_inplace_permuted(sdp_Mem* data, int is_forward,
+        sdp_Error* status);
+int sdp_fft_permuted_n2(int grid_size);
+
 #ifdef __cplusplus
 }
 #endif

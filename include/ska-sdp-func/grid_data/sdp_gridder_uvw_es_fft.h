@@ -90,6 +90,18 @@ double sdp_gridder_uvw_es_fft_beta(const sdp_GridderUvwEsFft* plan);
  * selects rocFFT + separate screen kernels instead), 0 for rocFFT. */
 int sdp_gridder_uvw_es_fft_fused_fft(const sdp_GridderUvwEsFft* plan);
 
+/* Calls are bucketed in batches of at most sdp_gridder_uvw_es_fft_batch_vis
+ * visibilities (whole rows): a larger call is split into row batches that
+ * are added into one grid (gridding) or gathered from one transformed grid
+ * (degridding), so bucketing indices stay 32-bit and the record scratch
+ * stays within SDP_ES_SCRATCH_GB (default 32 GiB). Results equal the
+ * unbatched call up to summation order. set_max_batch lowers the cap
+ * (0 = the default); a row with more channels than the cap is an invalid
+ * argument. */
+void sdp_gridder_uvw_es_fft_set_max_batch(sdp_GridderUvwEsFft* plan,
+        int64_t max_vis);
+int64_t sdp_gridder_uvw_es_fft_batch_vis(const sdp_GridderUvwEsFft* plan);
+
 /* Run the plan's work on a caller-owned hipStream_t (NULL = null stream). */
 void sdp_gridder_uvw_es_fft_set_stream(sdp_GridderUvwEsFft* plan,
         void* hip_stream);

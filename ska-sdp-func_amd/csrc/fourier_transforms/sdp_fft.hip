@@ -21,6 +21,7 @@
 #include "ska-sdp-func/fourier_transforms/sdp_fft.h"
 #include "ska-sdp-func/fourier_transforms/sdp_fft_padded_size.h"
 #include "ska-sdp-func/utility/sdp_logging.h"
+#include "../grid_data/es_fft.h"
 #include "../utility/sdp_hip.h"
 
 struct sdp_Fft
@@ -433,6 +434,38 @@ void sdp_fft_phase(sdp_Mem* data, sdp_Error* status)
 // sdp_fft_padded_size.cpp:87-126: the smallest even m >= ceil(n * factor)
 // whose half is 11-smooth (the reference walks a min-heap of 2 x products
 // of 2, 3, 5, 7, 11; this enumerates candidates directly).
+void sdp_fft_2d_inplace_permuted(sdp_Mem* data, int is_forward,
+        sdp_Error* status)
+{
+    if (*status) return;
+    const int64_t G = sdp_mem_num_dims(data) == 2 ?
+            sdp_mem_shape_dim(data, 0) : 0;
+    if (sdp_mem_type(data) != SDP_MEM_COMPLEX_FLOAT ||
+            sdp_mem_location(data) != SDP_MEM_GPU ||
+            sdp_mem_shape_dim(data, 1) != G || G > 16384 ||
+            !sdp_es::fused_fft_supported((int)G) ||
+            !sdp_mem_is_c_contiguous(data))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("sdp_fft_2d_inplace_permuted: a square complex-float "
+                "GPU array, side a power of two in [1024, 16384]");
+        return;
+    }
+    sdp_es::FftTwiddles tw;
+    int e = sdp_es::fft_twiddles_create((int)G, &tw);
+    if (!e)
+        e = sdp_es::fft2d_inplace_permuted((float*)sdp_mem_data(data),
+                (int)G, is_forward != 0, tw, 0);
+    if (!e) e = (int)hipStreamSynchronize(0) ? SDP_ERR_RUNTIME : 0;
+    sdp_es::fft_twiddles_destroy(&tw);
+    if (e) *status = (sdp_Error)e;
+}
+
+int sdp_fft_permuted_n2(int grid_size)
+{
+    return sdp_es::fft_perm_n2(grid_size);
+}
+
 int sdp_fft_padded_size(int n, double padding_factor)
 {
     const long long target = (long long)ceil(n * padding_factor);

@@ -112,10 +112,13 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
 
 // Grid-mode tile accumulation: writes every cell of the G x G grid, or
 // (skip_empty, f32 tap-table path) every cell of the tiles holding entries
-// -- for a consumer that reads the bin counts (fft_grid_rows_cols).
+// -- for a consumer that reads the bin counts (fft_grid_rows_cols). With
+// accumulate (one batch of a call split into batches), the tiles holding
+// entries are ADDED to the grid and nothing else is touched.
 template<typename T>
 int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
-        T* grid, hipStream_t stream, bool skip_empty = false);
+        T* grid, hipStream_t stream, bool skip_empty = false,
+        bool accumulate = false);
 
 // Degrid-mode tile gather: vis[idx] += sum_taps grid * kernel.
 template<typename T>

@@ -967,7 +967,8 @@ template<typename T, bool DO_W>
 __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
         const T* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
-        const uint32_t* __restrict__ item_bin, T* __restrict__ grid)
+        const uint32_t* __restrict__ item_bin, T* __restrict__ grid,
+        int accumulate)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int S = kScatterStride;
@@ -986,6 +987,7 @@ __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
     const uint32_t npieces = item_start[b + 1] - item_start[b];
     const uint32_t e0 = bin_start[b] + piece * kPiece;
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
+    if (accumulate && e0 == e1) return;     // nothing to add
     const int half = p.G / 2;
     int r0, c0;
     tile_origin(p, b, r0, c0);
@@ -1060,7 +1062,20 @@ __global__ __launch_bounds__(kThreads) void k_scatter(EsParams<T> p,
     __syncthreads();
 
     const int nr = min(kTile, p.G - r0), nc = min(kTile, p.G - c0);
-    if (npieces == 1)
+    if (npieces == 1 && accumulate)
+    {
+        // Batched call: this tile's only work item of the batch adds to
+        // the grid (no other writer during this launch).
+        for (int k = threadIdx.x; k < kTile * 2 * kTile; k += kThreads)
+        {
+            const int r = k / (2 * kTile), f = k - r * 2 * kTile;
+            const int c = f >> 1;
+            if (r >= nr || c >= nc) continue;
+            const T val = (f & 1) ? s_im[r * S + c] : s_re[r * S + c];
+            grid[((size_t)(r0 + r) * p.G + c0) * 2 + f] += val;
+        }
+    }
+    else if (npieces == 1)
     {
         // Plain stores: 2 cells (float) / 1 cell (double) = 16 B per lane.
         constexpr int kCells = sizeof(T) == 4 ? 2 : 1;
@@ -1195,7 +1210,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
         const uint32_t* __restrict__ item_bin, float* __restrict__ grid,
-        int skip_empty)
+        int flags)
 {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     static_assert(CHUNK == 128 || CHUNK == 256, "one or two threads per entry");
@@ -1221,7 +1236,12 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     const uint32_t npieces = item_start[b + 1] - item_start[b];
     const uint32_t e0 = bin_start[b] + piece * kPiece;
     const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
-    if (skip_empty && e0 == e1 && npieces == 1) return;
+    // flags bit 0 (skip_empty): a tile without entries is not written, its
+    // consumer reads the bin counts; bit 1 (accumulate): batched call, the
+    // tile is added to the grid (a work item without entries returns).
+    const bool accumulate = (flags & 2) != 0;
+    if ((flags & 1) && e0 == e1 && npieces == 1) return;
+    if (accumulate && e0 == e1) return;
     int r0, c0;
     tile_origin(p, b, r0, c0);
     if (r0 >= p.G || c0 >= p.G) return;
@@ -1417,7 +1437,14 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
             const int row = r0 + sub_r + kq * 4 + rr;
             if (row >= p.G || col >= p.G) continue;
             float* dst = grid + ((size_t)row * p.G + col) * 2;
-            if (npieces == 1)
+            if (npieces == 1 && accumulate)
+            {
+                float2 v = *(const float2*)dst;
+                v.x += acc_re[cblk][rr];
+                v.y += acc_im[cblk][rr];
+                *(float2*)dst = v;
+            }
+            else if (npieces == 1)
             {
                 float2 v;
                 v.x = acc_re[cblk][rr];
@@ -2173,20 +2200,24 @@ int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
 
 template<typename T>
 int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
-        T* grid, hipStream_t stream, bool skip_empty)
+        T* grid, hipStream_t stream, bool skip_empty, bool accumulate)
 {
     sdp_Error st = SDP_SUCCESS;
     sdp_Error* status = &st;
-    k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
-            p, s.item_start, grid);
-    SDP_HIP_CHECK_LAUNCH(status);
+    if (!accumulate)
+    {
+        k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
+                p, s.item_start, grid);
+        SDP_HIP_CHECK_LAUNCH(status);
+    }
+    const int acc = accumulate ? 1 : 0;
     // f32: the matrix-core tile kernels with per-entry tap tables (float
     // plans have W <= 16, sdp_gridder_uvw_es_fft_utils.cpp:498); f64 (and
     // any wider float support): LDS accumulation below.
     if constexpr (sizeof(T) == 4)
     {
         const float* recs = (const float*)s.recs;
-        const int se = skip_empty ? 1 : 0;
+        const int se = (skip_empty ? 1 : 0) | (accumulate ? 2 : 0);
         if (p.support <= 16)
         {
             if (p.support <= 8 && p.do_w)
@@ -2214,13 +2245,15 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     {
         SDP_HIP_CHECK(((hipError_t)allow_lds<k_scatter<T, true>>(lds)), status);
         k_scatter<T, true><<<n_items, kThreads, lds, stream>>>(
-                p, (const T*)s.recs, s.bin_start, s.item_start, s.item_bin, grid);
+                p, (const T*)s.recs, s.bin_start, s.item_start, s.item_bin, grid,
+                acc);
     }
     else
     {
         SDP_HIP_CHECK(((hipError_t)allow_lds<k_scatter<T, false>>(lds)), status);
         k_scatter<T, false><<<n_items, kThreads, lds, stream>>>(
-                p, (const T*)s.recs, s.bin_start, s.item_start, s.item_bin, grid);
+                p, (const T*)s.recs, s.bin_start, s.item_start, s.item_bin, grid,
+                acc);
     }
     SDP_HIP_CHECK_LAUNCH(status);
     return *status;
@@ -2348,7 +2381,7 @@ int reverse_screen(const ImageParams<T>& ip, int plane, T* dirty,
             const T*, const T*, const T*, BucketScratch*, hipStream_t, \
             uint32_t*, uint32_t*); \
     template int scatter<T>(const EsParams<T>&, const BucketScratch&, \
-            uint32_t, T*, hipStream_t, bool); \
+            uint32_t, T*, hipStream_t, bool, bool); \
     template int gather<T>(const EsParams<T>&, const BucketScratch&, \
             uint32_t, const T*, T*, hipStream_t); \
     template int screen_corr_2d<T>(const ImageParams<T>&, const T*, T*, \

@@ -8,6 +8,7 @@
 // bucketed by grid tile and scattered through LDS (es_kernels.hip), the FFT
 // is rocFFT with a plan cached in the gridder plan, and the image-plane
 // steps are fused (2-D: one kernel for screen + correction).
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -46,6 +47,7 @@ struct sdp_GridderUvwEsFft
     double inv_w_range;
     double conv_corr_norm_factor;
     int is_double;
+    int64_t max_batch_vis;      // caller's cap on visibilities per batch
 
     // Device state.
     void* grid;                 // G x G complex plane
@@ -191,6 +193,48 @@ size_t real_size(const sdp_GridderUvwEsFft* plan)
     return plan->is_double ? sizeof(double) : sizeof(float);
 }
 
+// Visibilities bucketed together (one batch). A call with more is split
+// into row batches whose tiles are added to the grid (gridding) or whose
+// visibilities are gathered from one transformed grid (degridding), so:
+//  * record indices stay 32-bit: a batch lists at most 4 entries per
+//    visibility (support <= 64 < tile), all below 2^32;
+//  * the two worst-case record arrays stay within SDP_ES_SCRATCH_GB
+//    (default 32 GiB) whatever the call size;
+//  * sdp_gridder_uvw_es_fft_set_max_batch lowers the cap (tests).
+int64_t batch_vis_limit(const sdp_GridderUvwEsFft* plan)
+{
+    static double scratch_gb = -1.0;
+    if (scratch_gb < 0.0)
+    {
+        const char* e = getenv("SDP_ES_SCRATCH_GB");
+        scratch_gb = e ? std::max(0.25, atof(e)) : 32.0;
+    }
+    const int64_t by_index = ((int64_t)1 << 30) - ((int64_t)1 << 20);
+    const double rec_bytes = (plan->do_wstacking ? 8.0 : 4.0) *
+            (plan->is_double ? 8.0 : 4.0);
+    const int64_t by_mem = (int64_t)(scratch_gb * 1073741824.0 /
+            (2.0 * 4.0 * rec_bytes));
+    int64_t lim = std::min(by_index, by_mem);
+    if (plan->max_batch_vis > 0) lim = std::min(lim, plan->max_batch_vis);
+    return std::max<int64_t>(1, lim);
+}
+
+// Rows per batch for num_chan channels (a row's channels stay together).
+int64_t rows_per_batch(const sdp_GridderUvwEsFft* plan, int num_chan,
+        sdp_Error* status)
+{
+    if (*status) return 1;
+    const int64_t lim = batch_vis_limit(plan);
+    if (num_chan > lim)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("%d channels exceed the %lld visibilities of one "
+                "bucketing batch", num_chan, (long long)lim);
+        return 1;
+    }
+    return std::max<int64_t>(1, lim / std::max(1, num_chan));
+}
+
 // (Re)allocate the bucketing count table for num_vis visibilities.
 void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
         sdp_Error* status)
@@ -239,19 +283,25 @@ void timing_mark(sdp_GridderUvwEsFft* plan, int k)
     if (plan->timing) (void)hipEventRecord(plan->ev[k], plan->stream);
 }
 
-// Sum the phase times of one plane into acc_ms (syncs the last event).
-// Interval k (event k -> k+1) is accumulated into slot[k]; slots are
-// 0 bucketing, 1 scatter/gather kernel, 2 FFT, 3 image-plane kernels.
-void timing_collect(sdp_GridderUvwEsFft* plan, const int slot[4])
+// Sum phase times into acc_ms (syncs event k1): interval k (event k ->
+// k + 1, k0 <= k < k1) is accumulated into slot[k]; slots are 0 bucketing,
+// 1 scatter/gather kernel, 2 FFT, 3 image-plane kernels.
+void timing_collect_range(sdp_GridderUvwEsFft* plan, int k0, int k1,
+        const int slot[4])
 {
     if (!plan->timing) return;
-    (void)hipEventSynchronize(plan->ev[4]);
-    for (int k = 0; k < 4; ++k)
+    (void)hipEventSynchronize(plan->ev[k1]);
+    for (int k = k0; k < k1; ++k)
     {
         float ms = 0.0f;
         (void)hipEventElapsedTime(&ms, plan->ev[k], plan->ev[k + 1]);
         plan->acc_ms[slot[k]] += ms;
     }
+}
+
+void timing_collect(sdp_GridderUvwEsFft* plan, const int slot[4])
+{
+    timing_collect_range(plan, 0, 4, slot);
 }
 
 const int kGridSlots[4] = {0, 1, 2, 3};     // bucket, scatter, fft, screen
@@ -306,7 +356,7 @@ sdp_es::ImageParams<T> image_params(const sdp_GridderUvwEsFft* plan)
 template<typename T>
 void scatter_plane(sdp_GridderUvwEsFft* plan, int plane, int64_t rows,
         int chan, const T* uvw, const T* freq, const T* vis, const T* weight,
-        T* grid, bool skip_empty, sdp_Error* status)
+        T* grid, bool skip_empty, bool accumulate, sdp_Error* status)
 {
     if (*status) return;
     const sdp_es::EsParams<T> p = es_params<T>(plan, plane);
@@ -317,7 +367,7 @@ void scatter_plane(sdp_GridderUvwEsFft* plan, int plane, int64_t rows,
     if (e) { *status = (sdp_Error)e; return; }
     timing_mark(plan, 1);
     e = sdp_es::scatter<T>(p, plan->scratch, n_items, grid, plan->stream,
-            skip_empty);
+            skip_empty, accumulate);
     if (e) { *status = (sdp_Error)e; return; }
     timing_mark(plan, 2);
 }
@@ -358,11 +408,35 @@ void grid_to_image(sdp_GridderUvwEsFft* plan,
     if (e) *status = (sdp_Error)e;
 }
 
-// Degridding: image (2-D: corrected in place) -> this plane's grid.
+// Gridding of rows [0, rows) in batches of rb rows into grid (zeroed
+// first): every batch's tiles are added (the FFT then reads the whole grid).
+template<typename T>
+void scatter_batches(sdp_GridderUvwEsFft* plan, int plane, int64_t rows,
+        int64_t rb, int chan, const T* uvw, const T* freq, const T* vis,
+        const T* weight, T* grid, sdp_Error* status)
+{
+    if (*status) return;
+    const size_t G = (size_t)plan->grid_size;
+    SDP_HIP_CHECK(hipMemsetAsync(grid, 0, G * G * 2 * real_size(plan),
+            plan->stream), status);
+    for (int64_t r0 = 0; r0 < rows && !*status; r0 += rb)
+    {
+        const int64_t n = std::min(rb, rows - r0);
+        scatter_plane<T>(plan, plane, n, chan, uvw + 3 * r0, freq,
+                vis + 2 * r0 * chan, weight + r0 * chan, grid, false, true,
+                status);
+        timing_collect_range(plan, 0, 2, kGridSlots);
+    }
+    timing_mark(plan, 2);
+}
+
+// Degridding: image (2-D: corrected in place) -> this plane's grid; tiles:
+// the bucketing's bin counts (only the tiles the gather reads are written)
+// or nullptr (every cell).
 template<typename T>
 void image_to_grid(sdp_GridderUvwEsFft* plan,
         const sdp_es::ImageParams<T>& ip, int plane, T* dirty, T* grid,
-        sdp_Error* status)
+        const uint32_t* tiles, sdp_Error* status)
 {
     if (*status) return;
     int e = 0;
@@ -377,9 +451,8 @@ void image_to_grid(sdp_GridderUvwEsFft* plan,
             if (e) { *status = (sdp_Error)e; return; }
             timing_mark(plan, 2);
             // Only the tiles this plane's gather reads are written.
-            e = sdp_es::fft_image_to_grid(ip, plan->fft_tw, grid,
-                    plan->scratch.bin_count, plan->ncoarse, real_form,
-                    plan->stream);
+            e = sdp_es::fft_image_to_grid(ip, plan->fft_tw, grid, tiles,
+                    plan->ncoarse, real_form, plan->stream);
             if (e) *status = (sdp_Error)e;
             return;
         }
@@ -396,16 +469,24 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
         const T* uvw, const T* freq, const T* vis, const T* weight, T* dirty,
         sdp_Error* status)
 {
-    ensure_scratch(plan, rows * chan, status);
+    const int64_t rb = rows_per_batch(plan, chan, status);
+    const bool batched = rows > rb;
+    ensure_scratch(plan, std::min(rows, rb) * chan, status);
     const sdp_es::ImageParams<T> ip = image_params<T>(plan);
     T* grid = (T*)plan->grid;
     for (int plane = 0; plane < plan->num_total_w_grids && !*status; ++plane)
     {
         // With the fused f32 FFT the empty tiles are neither written nor
-        // read (the row pass takes them from the bin counts as zeros).
-        const bool sparse = std::is_same<T, float>::value && plan->fused_fft;
-        scatter_plane<T>(plan, plane, rows, chan, uvw, freq, vis, weight,
-                grid, sparse, status);
+        // read (the row pass takes them from the bin counts as zeros); a
+        // batched call adds every batch to a zeroed grid instead.
+        const bool sparse = !batched && std::is_same<T, float>::value &&
+                plan->fused_fft;
+        if (batched)
+            scatter_batches<T>(plan, plane, rows, rb, chan, uvw, freq, vis,
+                    weight, grid, status);
+        else
+            scatter_plane<T>(plan, plane, rows, chan, uvw, freq, vis, weight,
+                    grid, sparse, false, status);
         grid_to_image<T>(plan, ip, plane, grid, dirty, sparse, status);
         if (*status) return;
         if (plan->do_wstacking && plane == plan->num_total_w_grids - 1)
@@ -414,7 +495,42 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
             if (e) { *status = (sdp_Error)e; return; }
         }
         timing_mark(plan, 4);
-        timing_collect(plan, kGridSlots);
+        timing_collect_range(plan, batched ? 2 : 0, 4, kGridSlots);
+    }
+}
+
+// Degridding of one plane in batches of rb rows: the image side writes
+// every grid cell once, then each batch is bucketed and gathered.
+template<typename T>
+void degrid_batches(sdp_GridderUvwEsFft* plan,
+        const sdp_es::ImageParams<T>& ip, int plane, int64_t rows,
+        int64_t rb, int chan, const T* uvw, const T* freq, T* vis, T* dirty,
+        sdp_Error* status)
+{
+    if (*status) return;
+    T* grid = (T*)plan->grid;
+    timing_mark(plan, 1);
+    image_to_grid<T>(plan, ip, plane, dirty, grid, nullptr, status);
+    if (*status) return;
+    timing_mark(plan, 3);
+    timing_collect_range(plan, 1, 3, kDegridSlots);
+    for (int64_t r0 = 0; r0 < rows; r0 += rb)
+    {
+        const int64_t n = std::min(rb, rows - r0);
+        const sdp_es::EsParams<T> p = es_params<T>(plan, plane);
+        uint32_t n_entries = 0, n_items = 0;
+        timing_mark(plan, 0);
+        int e = sdp_es::bucket<T>(p, sdp_es::MODE_DEGRID, n, chan,
+                uvw + 3 * r0, freq, nullptr, nullptr, &plan->scratch,
+                plan->stream, &n_entries, &n_items);
+        if (e) { *status = (sdp_Error)e; return; }
+        timing_mark(plan, 1);
+        e = sdp_es::gather<T>(p, plan->scratch, n_items, grid,
+                vis + 2 * r0 * chan, plan->stream);
+        if (e) { *status = (sdp_Error)e; return; }
+        timing_mark(plan, 2);
+        const int slots[4] = {0, 1, 0, 0};
+        timing_collect_range(plan, 0, 2, slots);
     }
 }
 
@@ -422,7 +538,9 @@ template<typename T>
 void run_degrid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
         const T* uvw, const T* freq, T* vis, T* dirty, sdp_Error* status)
 {
-    ensure_scratch(plan, rows * chan, status);
+    const int64_t rb = rows_per_batch(plan, chan, status);
+    const bool batched = rows > rb;
+    ensure_scratch(plan, std::min(rows, rb) * chan, status);
     if (*status) return;
     const sdp_es::ImageParams<T> ip = image_params<T>(plan);
     T* grid = (T*)plan->grid;
@@ -434,6 +552,12 @@ void run_degrid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
     }
     for (int plane = 0; plane < plan->num_total_w_grids && !*status; ++plane)
     {
+        if (batched)
+        {
+            degrid_batches<T>(plan, ip, plane, rows, rb, chan, uvw, freq,
+                    vis, dirty, status);
+            continue;
+        }
         const sdp_es::EsParams<T> p = es_params<T>(plan, plane);
         timing_mark(plan, 0);
         uint32_t n_entries = 0, n_items = 0;
@@ -442,7 +566,8 @@ void run_degrid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
                 &n_items);
         if (e) { *status = (sdp_Error)e; return; }
         timing_mark(plan, 1);
-        image_to_grid<T>(plan, ip, plane, dirty, grid, status);
+        image_to_grid<T>(plan, ip, plane, dirty, grid,
+                plan->scratch.bin_count, status);
         if (*status) return;
         timing_mark(plan, 3);
         e = sdp_es::gather<T>(p, plan->scratch, n_items, grid, vis,
@@ -627,8 +752,8 @@ sdp_GridderUvwEsFft* sdp_gridder_uvw_es_fft_create_plan(
             s.sb_start = s.totals + 2;
         }
     }
-    ensure_scratch(plan,
-            (int64_t)plan->num_rows * plan->num_chan, status);
+    ensure_scratch(plan, std::min((int64_t)plan->num_rows * plan->num_chan,
+            batch_vis_limit(plan)), status);
     // SDP_ES_FFT=rocfft keeps rocFFT + separate screen kernels for f32 too.
     const char* fft_env = getenv("SDP_ES_FFT");
     plan->fused_fft = !plan->is_double &&
@@ -825,18 +950,32 @@ void sdp_grid_uvw_es_fft_scatter(sdp_GridderUvwEsFft* plan,
     if (*status) return;
     const int64_t rows = sdp_mem_shape_dim(vis, 0);
     const int chan = (int)sdp_mem_shape_dim(vis, 1);
-    ensure_scratch(plan, rows * chan, status);
+    const int64_t rb = rows_per_batch(plan, chan, status);
+    ensure_scratch(plan, std::min(rows, rb) * chan, status);
     timing_begin(plan);
-    if (plan->is_double)
-        scatter_plane<double>(plan, 0, rows, chan,
-                *(const double* const*)p_uvw, *(const double* const*)p_freq,
-                *(const double* const*)p_vis, *(const double* const*)p_wt,
-                *(double**)p_grid, false, status);
-    else
-        scatter_plane<float>(plan, 0, rows, chan,
-                *(const float* const*)p_uvw, *(const float* const*)p_freq,
-                *(const float* const*)p_vis, *(const float* const*)p_wt,
-                *(float**)p_grid, false, status);
+#define SDP_ES_SPLIT(T) \
+    if (rows > rb) \
+        scatter_batches<T>(plan, 0, rows, rb, chan, *(const T* const*)p_uvw, \
+                *(const T* const*)p_freq, *(const T* const*)p_vis, \
+                *(const T* const*)p_wt, *(T**)p_grid, status); \
+    else \
+        scatter_plane<T>(plan, 0, rows, chan, *(const T* const*)p_uvw, \
+                *(const T* const*)p_freq, *(const T* const*)p_vis, \
+                *(const T* const*)p_wt, *(T**)p_grid, false, false, status);
+    if (plan->is_double) { SDP_ES_SPLIT(double) }
+    else { SDP_ES_SPLIT(float) }
+#undef SDP_ES_SPLIT
+}
+
+void sdp_gridder_uvw_es_fft_set_max_batch(sdp_GridderUvwEsFft* plan,
+        int64_t max_vis)
+{
+    if (plan) plan->max_batch_vis = max_vis > 0 ? max_vis : 0;
+}
+
+int64_t sdp_gridder_uvw_es_fft_batch_vis(const sdp_GridderUvwEsFft* plan)
+{
+    return plan ? batch_vis_limit(plan) : 0;
 }
 
 void sdp_grid_uvw_es_fft_finish(sdp_GridderUvwEsFft* plan, sdp_Mem* grid,

@@ -51,6 +51,19 @@ def fft_phase(data):
     Lib.sdp_fft_phase(Mem(data))
 
 
+def fft_2d_inplace_permuted(data, is_forward):
+    """MI355X extension: the w-stack plane FFT in place on a square
+    complex64 GPU array (side a power of two in [1024, 16384]); output row
+    k is stored at row N1 * (k % N2) + k // N2, N2 = fft_permuted_n2(G)."""
+    Lib.sdp_fft_2d_inplace_permuted(Mem(data), int(bool(is_forward)))
+
+
+def fft_permuted_n2(grid_size):
+    """N2 of sdp_fft_2d_inplace_permuted's row permutation (0: size not
+    supported)."""
+    return int(Lib.sdp_fft_permuted_n2(int(grid_size)))
+
+
 Lib.wrap_func(
     "sdp_fft_create",
     restype=Fft.handle_type(),
@@ -108,4 +121,17 @@ Lib.wrap_func(
         ctypes.c_int,
         ctypes.c_double,
     ],
+)
+
+Lib.wrap_func(
+    "sdp_fft_2d_inplace_permuted",
+    restype=None,
+    argtypes=[Mem.handle_type(), ctypes.c_int],
+    check_errcode=True,
+)
+
+Lib.wrap_func(
+    "sdp_fft_permuted_n2",
+    restype=ctypes.c_int,
+    argtypes=[ctypes.c_int],
 )

@@ -140,6 +140,16 @@ class GridderUvwEsFft(StructWrapper):
         power-of-two grid); False for rocFFT + separate screen kernels."""
         return bool(Lib.sdp_gridder_uvw_es_fft_fused_fft(self))
 
+    def set_max_batch(self, max_vis):
+        """Cap the visibilities bucketed together (0: the default cap);
+        larger calls run in row batches (MI355X extension)."""
+        Lib.sdp_gridder_uvw_es_fft_set_max_batch(self, int(max_vis))
+
+    @property
+    def batch_vis(self):
+        """Visibilities per bucketing batch (MI355X extension)."""
+        return int(Lib.sdp_gridder_uvw_es_fft_batch_vis(self))
+
     def set_stream(self, hip_stream_handle):
         """Launch on the given hipStream_t (int handle; 0 = null stream)."""
         Lib.sdp_gridder_uvw_es_fft_set_stream(
@@ -189,6 +199,10 @@ for _name in ("grid_size", "support", "num_w_planes"):
 Lib.wrap_func("sdp_gridder_uvw_es_fft_beta", restype=ctypes.c_double,
               argtypes=[_H])
 Lib.wrap_func("sdp_gridder_uvw_es_fft_fused_fft", restype=ctypes.c_int,
+              argtypes=[_H])
+Lib.wrap_func("sdp_gridder_uvw_es_fft_set_max_batch", restype=None,
+              argtypes=[_H, ctypes.c_int64])
+Lib.wrap_func("sdp_gridder_uvw_es_fft_batch_vis", restype=ctypes.c_int64,
               argtypes=[_H])
 Lib.wrap_func("sdp_gridder_uvw_es_fft_set_stream", restype=None,
               argtypes=[_H, ctypes.c_void_p])
