@@ -33,25 +33,17 @@ import numpy as np
 
 from . import es_params
 
+from . import _cc
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_BUILD = os.path.join(_HERE, "_build")
-_LIB = os.path.join(_BUILD, "libes_oracle.so")
 _lib = None
 
 
 def build(force=False):
-    """Compile oracle/es_oracle.c (gcc, OpenMP) into oracle/_build."""
-    src = os.path.join(_HERE, "es_oracle.c")
-    if (not force and os.path.exists(_LIB)
-            and os.path.getmtime(_LIB) >= os.path.getmtime(src)):
-        return _LIB
-    os.makedirs(_BUILD, exist_ok=True)
-    tmp = _LIB + f".tmp{os.getpid()}"
-    subprocess.check_call(["gcc", "-O2", "-fopenmp", "-fPIC", "-shared",
-                           "-fno-fast-math", "-ffp-contract=off", src,
-                           "-o", tmp, "-lm"])
-    os.replace(tmp, _LIB)
-    return _LIB
+    """Compile oracle/es_oracle.c (gcc, OpenMP) (oracle/_cc.py)."""
+    return _cc.shared("es_oracle.c", "libes_oracle.so",
+                      ["-O2", "-fopenmp", "-fno-fast-math", "-ffp-contract=off"],
+                      force)
 
 
 def lib():

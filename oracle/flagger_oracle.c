@@ -27,6 +27,14 @@
  * t == 0, where the reference discards the value).
  */
 #include <complex.h>
+/* glibc defines CMPLX / CMPLXF only for gcc >= 4.7; clang (the sanitizer
+ * build, oracle/_cc.py) has the same builtin. */
+#ifndef CMPLXF
+#define CMPLXF(x, y) __builtin_complex((float)(x), (float)(y))
+#endif
+#ifndef CMPLX
+#define CMPLX(x, y) __builtin_complex((double)(x), (double)(y))
+#endif
 #ifdef _OPENMP
 #include <omp.h>
 #endif

@@ -23,25 +23,18 @@ import numpy as np
 
 from . import wtower_oracle as wo
 
+from . import _cc
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_BUILD = os.path.join(_HERE, "_build")
-_LIB = os.path.join(_BUILD, "libwtower_port.so")
 _lib = None
 C_0 = 299792458.0
 
 
 def build(force=False):
-    """Compile oracle/wtower_port.c (gcc -O3, OpenMP) into oracle/_build."""
-    src = os.path.join(_HERE, "wtower_port.c")
-    if (not force and os.path.exists(_LIB)
-            and os.path.getmtime(_LIB) >= os.path.getmtime(src)):
-        return _LIB
-    os.makedirs(_BUILD, exist_ok=True)
-    tmp = _LIB + f".tmp{os.getpid()}"
-    subprocess.check_call(["gcc", "-O3", "-fcx-limited-range", "-fopenmp",
-                           "-fPIC", "-shared", src, "-o", tmp, "-lm"])
-    os.replace(tmp, _LIB)
-    return _LIB
+    """Compile oracle/wtower_port.c (gcc -O3, OpenMP) (oracle/_cc.py)."""
+    return _cc.shared("wtower_port.c", "libwtower_port.so",
+                      ["-O3", "-fcx-limited-range", "-fopenmp"],
+                      force)
 
 
 def lib():
