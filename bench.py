@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--c3-rows", type=int, default=10_000_000)
     ap.add_argument("--c3-chan", type=int, default=64)
     ap.add_argument("--c3-steps", type=int, default=3)
+    ap.add_argument("--no-wstack", action="store_true",
+                    help="skip the 3-D (w-stacking) line at the config-2 "
+                         "workload")
     ap.add_argument("--no-overlap", action="store_true",
                     help="multi-GPU: wait for each step's reduce before the "
                          "next step (default: reduce of step k overlaps "
@@ -215,12 +218,18 @@ def cpu_baseline(args, G, support, beta, uv_scale):
 
 def run_config3(args, torch, dev, dist, world, rank):
     """BASELINE config 3: 10M rows x 64 channels IN TOTAL, rows sharded
-    over the ranks, each rank scattering its shard into a private uv grid,
-    one RCCL reduce of the 8192^2 complex64 grids (512 MiB) onto rank 0,
-    then one FFT + screen + correction there (north star: reduce before the
-    FFT). With one GPU the whole call runs on it (no collective). A step
-    is one such sharded gridding of all 6.4e8 visibilities; the reduce is
-    also timed alone."""
+    over the ranks (strong scaling). Two ways to combine the ranks, both
+    timed at N > 1:
+      grid  -- the north star's form: each rank scatters its shard into a
+               private uv grid, one RCCL reduce of the 8192^2 complex64
+               grids (512 MiB) onto rank 0, one FFT + screen + correction
+               there;
+      image -- each rank runs the whole gridding call on its shard into a
+               partial image, one RCCL reduce of the 5440^2 f32 images
+               (118 MB) onto rank 0.
+    The top-level mvis_s / ms_per_step are the faster mode's. With one GPU
+    the whole call runs on it (no collective). Each reduce is also timed
+    alone (reduce_ms)."""
     from ska_sdp_func.grid_data import GridderUvwEsFft
     from ska_sdp_func.grid_data.distributed import grid_sharded, shard_rows
 
@@ -237,55 +246,150 @@ def run_config3(args, torch, dev, dist, world, rank):
     grid_buf = (torch.empty((G, G), dtype=torch.complex64, device=dev)
                 if world > 1 else None)
 
-    def step():
-        dirty.zero_()
-        if world == 1:
-            plan.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
-        else:
-            grid_sharded(plan, uvw, freq, vis, weight, dirty, dist,
-                         mode="grid", dst=0, grid_buf=grid_buf)
-
     def sync():
         torch.cuda.synchronize(dev)
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    step()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.c3_steps):
+    def timed(step):
         step()
-    sync()
-    t = time.perf_counter() - t0
-    reduce_ms = None
-    if dist is not None:
-        tt = torch.tensor([t], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t = float(tt.item())
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(args.c3_steps):
+            step()
+        sync()
+        t = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([t], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            t = float(tt.item())
+        return t
+
+    def reduce_ms(buf):
         n_red = 3
         sync()
         t0 = time.perf_counter()
         for _ in range(n_red):
-            dist.reduce(grid_buf, dst=0)
+            dist.reduce(buf, dst=0)
         sync()
-        reduce_ms = 1e3 * (time.perf_counter() - t0) / n_red
+        return round(1e3 * (time.perf_counter() - t0) / n_red, 3)
+
     total = args.c3_rows * args.c3_chan
+    modes = {}
+    if world == 1:
+        def step():
+            dirty.zero_()
+            plan.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
+        t = timed(step)
+        modes["single"] = {"mvis_s": round(total * args.c3_steps / t / 1e6,
+                                           3),
+                           "ms_per_step": round(1e3 * t / args.c3_steps, 3),
+                           "reduce_ms": None}
+    else:
+        for mode in ("grid", "image"):
+            def step(mode=mode):
+                dirty.zero_()
+                grid_sharded(plan, uvw, freq, vis, weight, dirty, dist,
+                             mode=mode, dst=0, grid_buf=grid_buf)
+            t = timed(step)
+            modes[mode] = {
+                "mvis_s": round(total * args.c3_steps / t / 1e6, 3),
+                "ms_per_step": round(1e3 * t / args.c3_steps, 3),
+                "reduce": ("RCCL reduce of the per-GPU 8192^2 complex64 "
+                           "grids (512 MiB) before one FFT on rank 0"
+                           if mode == "grid" else
+                           "RCCL reduce of the per-GPU partial images "
+                           f"({args.image}^2 f32, "
+                           f"{args.image ** 2 * 4 / 1e6:.0f} MB)"),
+                "reduce_ms": reduce_ms(grid_buf if mode == "grid"
+                                       else dirty),
+            }
+    best = max(modes, key=lambda k: modes[k]["mvis_s"])
     out = {
         "workload": (f"ES-FFT gridding, {args.c3_rows} rows x "
                      f"{args.c3_chan} chan in total (1.0-1.49 GHz), image "
                      f"{args.image}^2, eps {args.eps}, grid {G}^2, support "
-                     f"{plan.support}, rows sharded over {world} GPU(s)"),
-        "mvis_s": round(total * args.c3_steps / t / 1e6, 3),
-        "ms_per_step": round(1e3 * t / args.c3_steps, 3),
+                     f"{plan.support}, rows sharded over {world} GPU(s), "
+                     f"bucketing batches of {plan.batch_vis} visibilities"),
+        "mvis_s": modes[best]["mvis_s"],
+        "ms_per_step": modes[best]["ms_per_step"],
+        "best_mode": best,
+        "modes": modes,
         "steps": args.c3_steps,
         "scaling": "strong",
-        "reduce": ("RCCL reduce of the per-GPU 8192^2 complex64 grids "
-                   "(512 MiB) before one FFT on rank 0" if world > 1 else
-                   "none (one GPU)"),
-        "reduce_ms": round(reduce_ms, 3) if reduce_ms is not None else None,
     }
     del uvw, vis, weight, plan, grid_buf
+    torch.cuda.empty_cache()
+    return out
+
+
+def run_wstack(args, torch, dev, world, rank):
+    """3-D (w-stacking) ES gridding at the config-2 workload: the same 10M
+    rows x 1 channel with w +-500 m, image 5440^2, eps 1e-5 -> grid 8192^2,
+    W 8, do_w_stacking (ref sdp_gridder_uvw_es_fft.cpp:578-698): one
+    bucketing per call for all w-planes, then per plane the tile scatter
+    and the fused FFT with the w-screen; grid and degrid timed separately
+    (per GPU; no collective)."""
+    from ska_sdp_func.grid_data import GridderUvwEsFft
+
+    uvw, freq, vis, weight, px = make_inputs(
+        torch, dev, args.rows, args.chan, args.image, 20251015 + 2 + rank)
+    dirty = torch.zeros((args.image, args.image), dtype=torch.float32,
+                        device=dev)
+    plan = GridderUvwEsFft(uvw, freq, vis, weight, dirty, px, px, args.eps,
+                           True)
+    plan.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    steps = max(1, args.steps // 2)
+
+    def run(fn):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize(dev)
+        t = (time.perf_counter() - t0) / steps
+        plan.enable_timing(True)
+        fn()
+        tm = plan.get_timing()
+        plan.enable_timing(False)
+        return t, tm
+
+    def grid():
+        dirty.zero_()
+        plan.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
+
+    image0 = None
+    t_g, tm_g = run(grid)
+    image0 = dirty.clone()
+    out_vis = torch.zeros_like(vis)
+    img = torch.empty_like(dirty)
+
+    def degrid():
+        img.copy_(image0)
+        plan.ifft_grid_uvw_es(uvw, freq, out_vis, weight, img)
+
+    t_d, tm_d = run(degrid)
+    n = args.rows * args.chan
+    out = {
+        "workload": (f"ES-FFT 3-D (w-stacking), {args.rows} rows x "
+                     f"{args.chan} chan, w +-500 m, image {args.image}^2, "
+                     f"eps {args.eps}, grid {plan.grid_size}^2, support "
+                     f"{plan.support}, {plan.num_w_planes} w-planes"),
+        "w_planes": plan.num_w_planes,
+        "grid_mvis_s": round(n / t_g / 1e6, 3),
+        "grid_ms": round(1e3 * t_g, 3),
+        "grid_phases_ms": ({k: round(v, 4) for k, v in tm_g.items()}
+                           if tm_g else None),
+        "degrid_mvis_s": round(n / t_d / 1e6, 3),
+        "degrid_ms": round(1e3 * t_d, 3),
+        "degrid_phases_ms": ({k: round(v, 4) for k, v in tm_d.items()}
+                             if tm_d else None),
+        "steps": steps,
+    }
+    del uvw, vis, weight, plan, out_vis
     torch.cuda.empty_cache()
     return out
 
@@ -546,20 +650,33 @@ def main():
     config3 = None
     if not args.no_config3:
         config3 = run_config3(args, torch, dev, dist, world, rank)
+    wstack = None
+    if not args.no_wstack:
+        wstack = run_wstack(args, torch, dev, world, rank)
 
+    # CPU baselines on rank 0, after every GPU measurement (the other ranks
+    # wait at the final barrier). At N > 1 only the like-for-like ES port
+    # runs; the w-towers port (~1 min) only at N = 1.
     cpu = None
     cpu_wt = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(args, G, W, plan.beta, G * px)
         except Exception as exc:  # baseline failure must not hide the bench
             cpu = {"value": None, "unit": "Mvis/s", "cores": 0,
                    "kind": "port", "sample": f"failed: {exc!r}"}
-        try:
-            cpu_wt = cpu_baseline_wtower(args, uvw, freq, vis, px)
-        except Exception as exc:
-            cpu_wt = {"value": None, "unit": "Mvis/s", "cores": 0,
-                      "kind": "port", "sample": f"failed: {exc!r}"}
+        if world > 1 and cpu.get("value"):
+            # The job's value is all ranks' visibilities: the CPU baseline
+            # is per host (one CPU share), quoted beside it as measured.
+            cpu["note"] = (f"one host CPU share; compare with the per-GPU "
+                           f"rate {value / world:.1f} Mvis/s or the job's "
+                           f"{value:.1f}")
+        if world == 1:
+            try:
+                cpu_wt = cpu_baseline_wtower(args, uvw, freq, vis, px)
+            except Exception as exc:
+                cpu_wt = {"value": None, "unit": "Mvis/s", "cores": 0,
+                          "kind": "port", "sample": f"failed: {exc!r}"}
 
     if rank == 0:
         line = {
@@ -620,6 +737,7 @@ def main():
             "degrid": degrid,
             "grid_reduce_mode": grid_reduce,
             "config3": config3,
+            "wstack_3d": wstack,
             "roundtrip_mvis_s": (round(total_vis / ((ms_per_step
                                                      + degrid["ms_per_step"])
                                                     * 1e-3) / 1e6, 3)

@@ -100,10 +100,14 @@ bool super_geometry(int ntiles, int* sshift, int* nsuper, int* nsbins);
 // Bucketing, fully asynchronous: fills scratch.recs (sized by the caller
 // for the worst case, 4 entries per visibility) and the work-item table;
 // *n_items is the launch bound item_capacity (work items past the real
-// count find kNoBin and exit), *n_entries is 0. Record layouts:
+// count find kNoBin and exit), *n_entries is 0. 3-D (do_w): every
+// visibility is bucketed ONCE for all w-planes (p.plane is ignored), with
+// its plane coordinate pos_w in place of a w-tap; the tile kernels of
+// plane p derive the tap (plane_tap) and skip the records off that plane.
+// Record layouts:
 //   grid, 2-D:  {pu, pv, vre*w, vim*w}
-//   grid, 3-D:  {pu, pv, vre*w, vim*w*flip, kw, 0, 0, 0}
-//   degrid:     {pu, pv, kw*flip (sign carries flip), index bits}
+//   grid, 3-D:  {pu, pv, vre*w, vim*w*flip, pos_w, 0, 0, 0}
+//   degrid:     {pu, pv, flip (2-D) | pos_w*flip (3-D), index bits}
 template<typename T>
 int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
         const T* uvw, const T* freq, const T* vis, const T* weight,
@@ -121,9 +125,11 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         bool accumulate = false);
 
 // Degrid-mode tile gather: vis[idx] += sum_taps grid * kernel.
+// sort_records: reorder each work item's records by sub-tile first (f32,
+// W <= 8; once per bucketing -- later planes of a 3-D call reuse the order).
 template<typename T>
 int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
-        const T* grid, T* vis, hipStream_t stream);
+        const T* grid, T* vis, hipStream_t stream, bool sort_records = true);
 
 // Image-plane kernels. image N x N (real), grid G x G complex (interleaved).
 // conv_corr: [N/2+1] normalised separable correction; quad_*: Gauss-Legendre

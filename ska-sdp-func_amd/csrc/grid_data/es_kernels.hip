@@ -141,6 +141,15 @@ __device__ __forceinline__ bool footprint(const EsParams<T>& p, T u, T v,
     if (p.do_w)
     {
         const T pos_w = (w * inv_wavelength - p.min_plane_w) * p.w_scale;
+        if (p.plane < 0)
+        {
+            // Bucketing for every w-plane at once: the record keeps the
+            // plane coordinate (> 0: min_plane_w lies W / 2 - 1 planes
+            // below the smallest |w|); the tile kernel of plane p derives
+            // the w-tap (plane_tap) and skips the planes it misses.
+            f.kw = pos_w;
+            return f.u0 <= f.u1 && f.v0 <= f.v1;
+        }
         const int w0 = (int)ceil(pos_w - half_support);
         const int w1 = (int)floor(pos_w + half_support);
         if (p.plane < w0 || p.plane > w1) return false;
@@ -148,6 +157,24 @@ __device__ __forceinline__ bool footprint(const EsParams<T>& p, T u, T v,
         f.kw = es_tap(p.beta, (T)(p.plane - pos_w) * inv_half_support);
     }
     return f.u0 <= f.u1 && f.v0 <= f.v1;
+}
+
+// w-tap of plane p.plane for a record bucketed for all planes (its plane
+// coordinate pos_w, footprint() with p.plane < 0): the same arithmetic as
+// footprint(); false (tap 0) if the visibility does not touch the plane.
+template<typename T>
+__device__ __forceinline__ bool plane_tap(const EsParams<T>& p, T pos_w,
+        T& kw)
+{
+#pragma clang fp contract(off)
+    const T half_support = T(p.support) / T(2);
+    const int w0 = (int)ceil(pos_w - half_support);
+    const int w1 = (int)floor(pos_w + half_support);
+    kw = T(0);
+    if (p.plane < w0 || p.plane > w1) return false;
+    const T inv_half_support = T(1) / half_support;
+    kw = es_tap(p.beta, (T)(p.plane - pos_w) * inv_half_support);
+    return true;
 }
 
 // Clamped tap range from a record position (same formula as footprint()).
@@ -926,7 +953,7 @@ __device__ __forceinline__ void load_batch(const EsParams<T>& p,
         bt.pv = r[1];
         bt.a = r[2];
         bt.b = r[3];
-        if (DO_W) bt.kw = r[4];
+        if (DO_W) (void)plane_tap(p, r[4], bt.kw);   // 0 off this plane
     }
     int u1, v1;
     tap_range(p, bt.pu, bt.pv, bt.u0, u1, bt.v0, v1);
@@ -1284,12 +1311,17 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
         uint32_t rm = 0, cm = 0, pu16 = 0, pv16 = 0;
         const int eb = kLead + et * kStride;
+        bool on_plane = live;
         {
 #pragma clang fp contract(off)
             if (DO_W)
             {
-                r.z *= rw.x;
-                r.w *= rw.x;
+                // rw.x: the plane coordinate (bucketed for all planes);
+                // an entry off this w-plane gets no visits.
+                float kw = 0.0f;
+                on_plane = live && plane_tap(p, rw.x, kw);
+                r.z *= kw;
+                r.w *= kw;
             }
             u0 = max((int)ceilf(r.x - hs), gmin);
             if (stage_u)
@@ -1297,7 +1329,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 u1 = min((int)floorf(r.x + hs), gmax);
                 const int lo = max(u0 - tu0, 0) >> 4;
                 const int hi = min(u1 - tu0, kTile - 1) >> 4;
-                rm = live ? (2u << hi) - (1u << lo) : 0u;
+                rm = on_plane ? (2u << hi) - (1u << lo) : 0u;
                 pu16 = (uint32_t)(eb + 64 - (u0 - tu0));
             }
             if (stage_v)
@@ -1306,7 +1338,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 v1 = min((int)floorf(r.y + hs), gmax);
                 const int lo = max(v0 - tv0, 0) >> 4;
                 const int hi = min(v1 - tv0, kTile - 1) >> 4;
-                cm = live ? (2u << hi) - (1u << lo) : 0u;
+                cm = on_plane ? (2u << hi) - (1u << lo) : 0u;
                 pv16 = (uint32_t)(eb + 64 - (v0 - tv0));
             }
         }
@@ -1323,7 +1355,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
             info8[4 * et + (stage_u ? 0 : 1)] = (uint8_t)(stage_u ? rm : cm);
             pos16[2 * et + (stage_u ? 0 : 1)] = (uint16_t)(stage_u ? pu16 : pv16);
         }
-        if (live)
+        if (on_plane)
         {
 #pragma clang fp contract(off)
             if (stage_u)
@@ -1535,7 +1567,12 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         int wlo_r = 1, whi_r = 0, wlo_c = 1, whi_c = 0;
         int u0 = 0, u1 = -1, v0 = 0, v1 = -1;
         uint32_t pk = 0;
-        if (t < n)
+        // 3-D: records carry the plane coordinate (|r.z|); an entry off
+        // this w-plane gets no visits and no write-back.
+        float kw = 1.0f;
+        const bool on_plane = t < n &&
+                (!DO_W || plane_tap(p, fabsf(r.z), kw));
+        if (on_plane)
         {
             tap_range(p, r.x, r.y, u0, u1, v0, v1);
             wlo_r = (u0 - tu0) >> 4;
@@ -1549,7 +1586,7 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         pool_count<kSub>(s_pc, lane, wave, wlo_r, whi_r, wlo_c, whi_c, sub,
                 rank);
         __syncthreads();   // B1: previous chunk consumed
-        if (t < n)
+        if (on_plane)
         {
 #pragma clang fp contract(off)
             float tu[NTAP], tv[NTAP];
@@ -1562,7 +1599,6 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
                 s_kv[t * NTAP + d] = tv[d];
             }
             // (-1)^(u0 + v0) of the checkerboard, with the w-tap
-            const float kw = DO_W ? fabsf(r.z) : 1.0f;
             s_kw[t] = ((u0 + v0) & 1) ? -kw : kw;
         }
         s_acc_re[t] = 0.0f;
@@ -1645,7 +1681,7 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
             }
         }
         __syncthreads();
-        if (t < n)
+        if (on_plane)
         {
             const uint64_t idx = (uint64_t)__float_as_uint(r.w);
             const float flip = signbit(r.z) ? -1.0f : 1.0f;
@@ -1816,7 +1852,10 @@ __global__ __launch_bounds__(kThreads) void k_gather(EsParams<T> p,
         Batch<T> bt;
         // Gather records are {pu, pv, kw*flip, index}: kw = |a|.
         load_batch<T, false, 4>(p, recs, base, e1, lane, tu0, tv0, wrows, bt);
-        const T kw_lane = fabs(bt.a);
+        // 3-D: |a| is the plane coordinate (bucketed for all planes).
+        const T pw = fabs(bt.a);
+        T kw_lane = pw;
+        if (DO_W) (void)plane_tap(p, pw, kw_lane);   // 0 off this plane
         T res_re = T(0), res_im = T(0);
         for (int g = 0; g < bt.cnt; g += 4)
         {
@@ -2128,11 +2167,14 @@ void launch_fill(int nc, int64_t chunk, const EsParams<T>& p,
     }
 
 template<typename T>
-int bucket(const EsParams<T>& p, Mode mode, int64_t num_rows, int num_chan,
+int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
         const T* uvw, const T* freq, const T* vis, const T* weight,
         BucketScratch* s, hipStream_t stream, uint32_t* n_entries,
         uint32_t* n_items)
 {
+    // 3-D: all w-planes at once (records keep pos_w, footprint()).
+    EsParams<T> p = p_in;
+    if (p.do_w) p.plane = -1;
     sdp_Error st = SDP_SUCCESS;
     sdp_Error* status = &st;
     const int64_t num_vis = num_rows * num_chan;
@@ -2274,7 +2316,7 @@ bool sort_pieces()
 
 template<typename T>
 int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
-        const T* grid, T* vis, hipStream_t stream)
+        const T* grid, T* vis, hipStream_t stream, bool sort_records)
 {
     sdp_Error st = SDP_SUCCESS;
     sdp_Error* status = &st;
@@ -2283,7 +2325,7 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         const float* recs = (const float*)s.recs;
         if (p.support <= 16)
         {
-            if (p.support <= 8 && sort_pieces())
+            if (p.support <= 8 && sort_records && sort_pieces())
             {
                 k_sort_pieces<<<n_items, 256, 0, stream>>>(p,
                         (float*)s.recs, s.bin_start, s.item_start,
@@ -2383,7 +2425,7 @@ int reverse_screen(const ImageParams<T>& ip, int plane, T* dirty,
     template int scatter<T>(const EsParams<T>&, const BucketScratch&, \
             uint32_t, T*, hipStream_t, bool, bool); \
     template int gather<T>(const EsParams<T>&, const BucketScratch&, \
-            uint32_t, const T*, T*, hipStream_t); \
+            uint32_t, const T*, T*, hipStream_t, bool); \
     template int screen_corr_2d<T>(const ImageParams<T>&, const T*, T*, \
             hipStream_t); \
     template int screen_accumulate<T>(const ImageParams<T>&, int, const T*, \

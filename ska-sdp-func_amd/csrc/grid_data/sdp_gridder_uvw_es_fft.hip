@@ -299,11 +299,6 @@ void timing_collect_range(sdp_GridderUvwEsFft* plan, int k0, int k1,
     }
 }
 
-void timing_collect(sdp_GridderUvwEsFft* plan, const int slot[4])
-{
-    timing_collect_range(plan, 0, 4, slot);
-}
-
 const int kGridSlots[4] = {0, 1, 2, 3};     // bucket, scatter, fft, screen
 const int kDegridSlots[4] = {0, 3, 2, 1};   // bucket, screen, fft, gather
 
@@ -472,21 +467,44 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
     const int64_t rb = rows_per_batch(plan, chan, status);
     const bool batched = rows > rb;
     ensure_scratch(plan, std::min(rows, rb) * chan, status);
+    if (*status) return;
     const sdp_es::ImageParams<T> ip = image_params<T>(plan);
     T* grid = (T*)plan->grid;
+    // With the fused f32 FFT the empty tiles are neither written nor read
+    // (the row pass takes them from the bin counts as zeros); a batched
+    // call adds every batch to a zeroed grid instead.
+    const bool sparse = !batched && std::is_same<T, float>::value &&
+            plan->fused_fft;
+    uint32_t n_items = 0;
+    if (!batched)
+    {
+        // One bucketing for the call: 3-D records carry their plane
+        // coordinate and serve every w-plane (es_kernels.h, bucket).
+        uint32_t n_entries = 0;
+        timing_mark(plan, 0);
+        const int e = sdp_es::bucket<T>(es_params<T>(plan, 0),
+                sdp_es::MODE_GRID, rows, chan, uvw, freq, vis, weight,
+                &plan->scratch, plan->stream, &n_entries, &n_items);
+        if (e) { *status = (sdp_Error)e; return; }
+        timing_mark(plan, 1);
+        timing_collect_range(plan, 0, 1, kGridSlots);
+    }
     for (int plane = 0; plane < plan->num_total_w_grids && !*status; ++plane)
     {
-        // With the fused f32 FFT the empty tiles are neither written nor
-        // read (the row pass takes them from the bin counts as zeros); a
-        // batched call adds every batch to a zeroed grid instead.
-        const bool sparse = !batched && std::is_same<T, float>::value &&
-                plan->fused_fft;
         if (batched)
+        {
             scatter_batches<T>(plan, plane, rows, rb, chan, uvw, freq, vis,
                     weight, grid, status);
+        }
         else
-            scatter_plane<T>(plan, plane, rows, chan, uvw, freq, vis, weight,
-                    grid, sparse, false, status);
+        {
+            timing_mark(plan, 1);
+            const int e = sdp_es::scatter<T>(es_params<T>(plan, plane),
+                    plan->scratch, n_items, grid, plan->stream, sparse,
+                    false);
+            if (e) { *status = (sdp_Error)e; return; }
+            timing_mark(plan, 2);
+        }
         grid_to_image<T>(plan, ip, plane, grid, dirty, sparse, status);
         if (*status) return;
         if (plan->do_wstacking && plane == plan->num_total_w_grids - 1)
@@ -495,7 +513,7 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
             if (e) { *status = (sdp_Error)e; return; }
         }
         timing_mark(plan, 4);
-        timing_collect_range(plan, batched ? 2 : 0, 4, kGridSlots);
+        timing_collect_range(plan, batched ? 2 : 1, 4, kGridSlots);
     }
 }
 
@@ -550,6 +568,19 @@ void run_degrid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
         e = sdp_es::apply_correction<T>(ip, dirty, plan->stream);
         if (e) { *status = (sdp_Error)e; return; }
     }
+    uint32_t n_items = 0;
+    if (!batched)
+    {
+        // One bucketing for the call (3-D: for every w-plane).
+        uint32_t n_entries = 0;
+        timing_mark(plan, 0);
+        e = sdp_es::bucket<T>(es_params<T>(plan, 0), sdp_es::MODE_DEGRID,
+                rows, chan, uvw, freq, nullptr, nullptr, &plan->scratch,
+                plan->stream, &n_entries, &n_items);
+        if (e) { *status = (sdp_Error)e; return; }
+        timing_mark(plan, 1);
+        timing_collect_range(plan, 0, 1, kDegridSlots);
+    }
     for (int plane = 0; plane < plan->num_total_w_grids && !*status; ++plane)
     {
         if (batched)
@@ -558,23 +589,17 @@ void run_degrid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
                     vis, dirty, status);
             continue;
         }
-        const sdp_es::EsParams<T> p = es_params<T>(plan, plane);
-        timing_mark(plan, 0);
-        uint32_t n_entries = 0, n_items = 0;
-        e = sdp_es::bucket<T>(p, sdp_es::MODE_DEGRID, rows, chan, uvw, freq,
-                nullptr, nullptr, &plan->scratch, plan->stream, &n_entries,
-                &n_items);
-        if (e) { *status = (sdp_Error)e; return; }
         timing_mark(plan, 1);
         image_to_grid<T>(plan, ip, plane, dirty, grid,
                 plan->scratch.bin_count, status);
         if (*status) return;
         timing_mark(plan, 3);
-        e = sdp_es::gather<T>(p, plan->scratch, n_items, grid, vis,
-                plan->stream);
+        // The records are sorted for the gather once per bucketing.
+        e = sdp_es::gather<T>(es_params<T>(plan, plane), plan->scratch,
+                n_items, grid, vis, plan->stream, plane == 0);
         if (e) { *status = (sdp_Error)e; return; }
         timing_mark(plan, 4);
-        timing_collect(plan, kDegridSlots);
+        timing_collect_range(plan, 1, 4, kDegridSlots);
     }
 }
 
