@@ -31,3 +31,19 @@ for r in csv.DictReader(open(sys.argv[1])):
     m = re.search(r"(k_[a-z_0-9]+(<[^>(]*>)?)", r["Name"])
     if m: print(f'{m.group(1)[:50]:50s} {float(r["AverageNs"])/1e3:9.1f} us x {r["Calls"]}')
 PY
+# Optional A/B: kernel traces of library variants (name:dir ...) after it.
+if [ -n "$AB" ]; then
+    scripts/kt_variants.sh "$OUT/ab" $AB || exit 1
+    for spec in $AB; do
+        n=${spec%%:*}
+        f=$(find "$OUT/ab/$n" -name "*kernel_stats.csv" | head -1)
+        echo "== $n"
+        python3 - "$f" <<'PY'
+import csv, re, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    m = re.search(r"(k_[a-z_0-9]+(<[^>(]*>)?)", r["Name"])
+    if m and float(r["AverageNs"]) > 20e3:
+        print(f'{m.group(1)[:50]:50s} {float(r["AverageNs"])/1e3:9.1f} us x {r["Calls"]}')
+PY
+    done
+fi

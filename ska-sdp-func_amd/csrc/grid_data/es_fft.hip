@@ -13,6 +13,7 @@
 // Column passes: B = 256 / P adjacent columns per workgroup (B * 8 bytes
 // contiguous per row access: 256 B at L = 128, 512 B at L = 64), LDS index
 // e * B + column.
+#include <algorithm>
 #include <cmath>
 #include <utility>
 #include <vector>
@@ -878,6 +879,165 @@ k_rows_herm(float2* __restrict__ grid, int k0, int M,
     }
 }
 
+// Single-row form of the real-output row pass (SDP_ES_HERM_ROWS=1): one
+// H row per iteration, H[u] = (A[u] + conj A[-u](-v)) / 2 for u = 0 .. G/2,
+// transformed and written as Bh[u] (M centre columns) into grid row u. A
+// workgroup is one row's threads and LDS (RowPlan<G>), so two share a CU and
+// one's loads overlap the other's transform (the quad form holds both rows
+// of a pair in one 1024-thread workgroup, one per CU). Grid rows u and G - u
+// are read only by row u's iteration, so the pass stays in place. The pair
+// mixing Z = Xe + i Xo moves into the first column pass
+// (k_cols_a_herm_pairs).
+template<int G>
+__global__ void __launch_bounds__(RowPlan<G>::P)
+k_rows_herm1(float2* __restrict__ grid, int k0, int M,
+        const float2* __restrict__ W, const uint32_t* __restrict__ occ)
+{
+    using F = RowFft<G, 1>;
+    constexpr int P = RowPlan<G>::P, EPT = F::EPT;
+    constexpr int NC = occ_classes(G), NH = G / 2 + 1;
+    static_assert(EPT == 16 && P == G / 16 && P % 64 == 0,
+            "element r of thread p at column p + r P (k_row_occupancy)");
+    extern __shared__ float2 lds[];
+    const int p = threadIdx.x;
+    const Buf gb(grid - k0, grid_bytes(G, k0));
+    F f;
+    f.init(p, W, G);
+    const int per = (NH + gridDim.x - 1) / gridDim.x;
+    const int u_begin = blockIdx.x * per, u_end = min(NH, u_begin + per);
+    for (int u = u_begin; u < u_end; ++u)
+    {
+        const int pq = opaque(p);
+        const int ur = (G - u) & (G - 1);
+        const uint32_t oa_bits = occ ?
+                occ[(u >> 6) * NC + (pq >> 6)] : 0xFFFFFFFFu;
+        const uint32_t ob_bits = occ ?
+                occ[(ur >> 6) * NC + ((pq + 63) >> 6)] >> 16 : 0xFFFFFFFFu;
+        const uint32_t ra = ((uint32_t)u * G + k0) * 8u;
+        const uint32_t rb = ((uint32_t)ur * G + k0) * 8u;
+        float2 v[EPT];
+        F::load_input(v, [&](int c) {
+            const int ca = pq + c, cb = (G - ca) & (G - 1);
+            const bool oa = (oa_bits >> (c / P)) & 1u;
+            const bool ob = (ob_bits >> (c / P)) & 1u;
+            const float2 a = gb.load_if(oa, ra + (uint32_t)ca * 8u);
+            const float2 b = gb.load_if(ob, rb + (uint32_t)cb * 8u);
+            return make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
+        });
+        f.transform(v, pq, lds, RowIdx{});
+        const uint32_t vr = (uint32_t)u * G * 8u + (uint32_t)pq * 8u;
+        F::store_output(v, [&](int c, int, float2 x) {
+            gb.store_if((unsigned)(pq + c - k0) < (unsigned)M, x, vr + c * 8u);
+        });
+    }
+}
+
+// Column pass A of the half-length transform on the Bh rows of
+// k_rows_herm1: it first forms the Z rows, Z[m] = (Bh[m] + conj Bh[G/2 - m])
+// + i (Bh[m] - conj Bh[G/2 - m]) e^{2 pi i m / G}, then runs k_cols_a_herm's
+// length-N2 transforms. Rows m = u1 + N1 n2 (class u1) pair with rows of
+// class N1 - u1 (element N2 - 1 - n2), so workgroup j takes the classes j
+// and N1 - j together (j = 0: class 0 alone, whose element n2 pairs with
+// N2 - n2 and element 0 with Bh[G/2]; j = N1/2: class N1/2 alone); the
+// partner values are exchanged through LDS.
+template<int N2>
+constexpr size_t cols_pair_lds_bytes()
+{
+    return std::max(kColLdsBytes,
+            (size_t)(N2 + 1) * ColPlan<N2>::B * sizeof(float2));
+}
+
+template<int N1, int N2>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_COLA_WAVES)))
+k_cols_a_herm_pairs(float2* __restrict__ grid, int M,
+        const float2* __restrict__ W)
+{
+    constexpr int G = 2 * N1 * N2, B = ColPlan<N2>::B, PT = ColPlan<N2>::P;
+    using F = ColFft<N2, 1>;
+    static_assert(F::EPT == 16 && PT * 16 == N2, "element n2 = p + PT r");
+    extern __shared__ float2 lds[];
+    const int c = threadIdx.x % B, p = threadIdx.x / B;
+    const int ja = blockIdx.x, jb = (N1 - ja) & (N1 - 1);
+    const bool pair = ja != jb;
+    const Buf gb(grid, grid_bytes(G, 0));
+    F f;
+    f.init(p, W, G);
+    const int ncb = (M + B - 1) / B;
+    constexpr uint32_t kStep = (uint32_t)N1 * G * 8u;   // one n2 / k2 step
+    const uint32_t so_a = (uint32_t)ja * G * 8u, so_b = (uint32_t)jb * G * 8u;
+    // Z of class u1 from its own Bh values v and the partners' from LDS
+    // (rows n2' of the class the LDS holds).
+    auto form_z = [&](float2 (&v)[16], int u1, bool self0, int cq) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+        {
+            const int n2 = p + PT * r;
+            const int n2p = self0 ? N2 - n2 : N2 - 1 - n2;
+            const float2 b = lds[n2p * B + cq];
+            const float2 a = v[r];
+            const float2 wt = W[u1 + N1 * n2];
+            const float2 w = make_float2(wt.x, -wt.y);    // e^{2 pi i m / G}
+            const float2 xe = make_float2(a.x + b.x, a.y - b.y);
+            const float2 xo = cmul(make_float2(a.x - b.x, a.y + b.y), w);
+            v[r] = make_float2(xe.x - xo.y, xe.y + xo.x);
+        }
+    };
+    auto to_lds = [&](const float2 (&v)[16], int cq) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) lds[(p + PT * r) * B + cq] = v[r];
+    };
+    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
+    {
+        const int pq = opaque(p), cq = opaque(c);
+        const int col = cb * B + cq;
+        const bool ok = col < M;
+        const uint32_t vo = ((uint32_t)pq * N1 * G + col) * 8u;
+        float2 va[16], vb[16];
+        F::load_input(va, [&](int e) {
+            return ok ? gb.load(vo, so_a + e * kStep) : make_float2(0.f, 0.f);
+        });
+        if (pair)
+            F::load_input(vb, [&](int e) {
+                return ok ? gb.load(vo, so_b + e * kStep)
+                          : make_float2(0.f, 0.f);
+            });
+        // Class 0's element 0 pairs with Bh[G/2] (row N1 N2).
+        float2 xrow = make_float2(0.f, 0.f);
+        if (ja == 0 && p == 0 && ok)
+            xrow = gb.load(((uint32_t)N1 * N2 * G + col) * 8u, 0);
+        __syncthreads();                 // previous transform's LDS use done
+        if (pair) to_lds(vb, cq);
+        else to_lds(va, cq);
+        if (ja == 0 && p == 0) lds[N2 * B + cq] = xrow;
+        __syncthreads();
+        float2 za[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) za[r] = va[r];
+        form_z(za, ja, ja == 0, cq);
+        if (pair)
+        {
+            __syncthreads();
+            to_lds(va, cq);
+            __syncthreads();
+            form_z(vb, jb, false, cq);
+        }
+        __syncthreads();                 // partners read: LDS free
+        f.transform(za, pq, lds, ColIdx<B>{cq});
+        F::store_output(za, [&](int e, int i, float2 x) {
+            const float2 fs = F::twiddle(W, 2 * ja * F::out_index(pq, i));
+            if (ok) gb.store(cmul(x, fs), vo, so_a + e * kStep);
+        });
+        if (pair)
+        {
+            f.transform(vb, pq, lds, ColIdx<B>{cq});
+            F::store_output(vb, [&](int e, int i, float2 x) {
+                const float2 fs = F::twiddle(W, 2 * jb * F::out_index(pq, i));
+                if (ok) gb.store(cmul(x, fs), vo, so_b + e * kStep);
+            });
+        }
+    }
+}
+
 // Column pass A of the half-length transform: for u1 = blockIdx.x,
 // length-N2 FFTs over the Z rows u1 + N1 * n2 (row pitch G = 2 N1 N2),
 // times e^{2 pi i u1 k2 / (G/2)}, back into rows u1 + N1 * k2.
@@ -1323,6 +1483,150 @@ k_cols_b_image_herm(float2* __restrict__ grid, int M,
     }
 }
 
+// Column pass B (forward) of the half-length transform in the single-row
+// form (SDP_ES_HERM_ROWS=1): after the length-N1 transforms it recovers
+// the column spectra X[k] = (Z[k] + conj Z[G/2 - k]) / 2 - i (Z[k] - conj
+// Z[G/2 - k]) e^{-2 pi i k / G} / 2 itself and writes X[k] into row k
+// (k in [0, G/2]; X[G/2] from Z[0]), so the row pass takes one row per
+// workgroup iteration (k_rows_image_herm1). Z rows k = k2 + N2 k1 of class
+// k2 pair with class N2 - k2 (element N1 - 1 - k1); workgroup j takes the
+// classes j and N2 - j (j = 0: class 0 alone, element k1 paired with
+// N1 - k1 mod N1; j = N2/2 alone); partners are exchanged through LDS.
+template<int N1, int N2>
+__global__ void __launch_bounds__(256)
+k_cols_b_image_herm_pairs(float2* __restrict__ grid, int M,
+        const float2* __restrict__ W)
+{
+    constexpr int G = 2 * N1 * N2, B = ColPlan<N1>::B;
+    using F = ColFft<N1, -1>;
+    static_assert(F::EPT == 16 && (size_t)N1 * B * sizeof(float2) <=
+            kColLdsBytes, "partner exchange fits the transform's LDS");
+    extern __shared__ float2 lds[];
+    const int c = threadIdx.x % B, p = threadIdx.x / B;
+    const int ja = blockIdx.x, jb = (N2 - ja) & (N2 - 1);
+    const bool pair = ja != jb;
+    const Buf gb(grid, grid_bytes(G, 0));
+    F f;
+    f.init(p, W, G);
+    const int ncb = (M + B - 1) / B;
+    constexpr uint32_t kStep = (uint32_t)N2 * G * 8u;
+    const uint32_t so_a = (uint32_t)ja * G * 8u, so_b = (uint32_t)jb * G * 8u;
+    auto to_lds = [&](const float2 (&v)[16], int pq, int cq) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lds[F::out_index(pq, i) * B + cq] = v[i];
+    };
+    // X of class k2 from its own Z values and the partners' in LDS.
+    auto form_x = [&](float2 (&v)[16], int k2, bool self0, int pq, int cq) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+        {
+            const int k1 = F::out_index(pq, i);
+            const int k1p = self0 ? (N1 - k1) & (N1 - 1) : N1 - 1 - k1;
+            const float2 a = v[i], b = lds[k1p * B + cq];
+            const float2 w = W[k2 + N2 * k1];            // e^{-2 pi i k / G}
+            const float2 dw = cmul(make_float2(a.x - b.x, a.y + b.y), w);
+            v[i] = make_float2(0.5f * ((a.x + b.x) + dw.y),
+                    0.5f * ((a.y - b.y) - dw.x));
+        }
+    };
+    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
+    {
+        const int pq = opaque(p), cq = opaque(c);
+        const int col = cb * B + cq;
+        const bool ok = col < M;
+        const uint32_t vo = ((uint32_t)pq * N2 * G + col) * 8u;
+        float2 va[16], vb[16];
+        F::load_input(va, [&](int e) {
+            return ok ? gb.load(vo, so_a + e * kStep) : make_float2(0.f, 0.f);
+        });
+        if (pair)
+            F::load_input(vb, [&](int e) {
+                return ok ? gb.load(vo, so_b + e * kStep)
+                          : make_float2(0.f, 0.f);
+            });
+        f.transform(va, pq, lds, ColIdx<B>{cq});
+        if (pair) f.transform(vb, pq, lds, ColIdx<B>{cq});
+        __syncthreads();                 // transforms' LDS use done
+        to_lds(pair ? vb : va, pq, cq);
+        __syncthreads();
+        // Z[0] (class 0, element 0) also gives X[G/2] (partner Z[0],
+        // e^{-i pi} = -1), written into row G/2.
+        float2 z0 = va[0];
+        float2 xa[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) xa[i] = va[i];
+        form_x(xa, ja, ja == 0, pq, cq);
+        if (pair)
+        {
+            __syncthreads();
+            to_lds(va, pq, cq);
+            __syncthreads();
+            form_x(vb, jb, false, pq, cq);
+        }
+        const uint32_t vs = ((uint32_t)pq * N2 * G + col) * 8u;
+        F::store_output(xa, [&](int e, int, float2 x) {
+            if (ok) gb.store(x, vs, so_a + e * kStep);
+        });
+        if (pair)
+            F::store_output(vb, [&](int e, int, float2 x) {
+                if (ok) gb.store(x, vs, so_b + e * kStep);
+            });
+        if (ja == 0 && pq == 0 && ok && F::out_index(0, 0) == 0)
+        {
+            const float2 dw = cmul(make_float2(0.0f, z0.y + z0.y),
+                    make_float2(-1.0f, 0.0f));
+            const float2 x = make_float2(0.5f * ((z0.x + z0.x) + dw.y),
+                    0.5f * (0.0f - dw.x));
+            gb.store(x, ((uint32_t)(G / 2) * G + col) * 8u, 0);
+        }
+    }
+}
+
+// Row pass (forward) of the real-input form, single-row: X row u (u in
+// [0, G/2], from k_cols_b_image_herm_pairs) transformed along the row and
+// written as grid row u and row G - u (conjugate, reversed). Row u is read
+// only by its own iteration and rows above G/2 by nobody, so in place.
+template<int G>
+__global__ void __launch_bounds__(RowPlan<G>::P)
+k_rows_image_herm1(float2* __restrict__ grid, int k0, int M,
+        const float2* __restrict__ W, const uint32_t* __restrict__ need)
+{
+    using F = RowFft<G, -1>;
+    constexpr int P = RowPlan<G>::P, EPT = F::EPT;
+    constexpr int NC = occ_classes(G), NH = G / 2 + 1;
+    static_assert(EPT == 16 && P == G / 16 && P % 64 == 0,
+            "element r of thread p at column p + r P (k_row_occupancy)");
+    extern __shared__ float2 lds[];
+    const int p = threadIdx.x;
+    const Buf gb(grid - k0, grid_bytes(G, k0));
+    F f;
+    f.init(p, W, G);
+    const int per = (NH + gridDim.x - 1) / gridDim.x;
+    const int u_begin = blockIdx.x * per, u_end = min(NH, u_begin + per);
+    for (int u = u_begin; u < u_end; ++u)
+    {
+        const int pq = opaque(p);
+        float2 v[EPT];
+        const uint32_t vx = (uint32_t)u * G * 8u + (uint32_t)pq * 8u;
+        F::load_input(v, [&](int c) {
+            return gb.load_if((unsigned)(pq + c - k0) < (unsigned)M, vx + c * 8u);
+        });
+        f.transform(v, pq, lds, RowIdx{});
+        const int ur = (G - u) & (G - 1);
+        const uint32_t nf = need ? need[(u >> 6) * NC + (pq >> 6)] : ~0u;
+        const uint32_t nr = need ?
+                need[(ur >> 6) * NC + ((pq + 63) >> 6)] >> 16 : ~0u;
+        const uint32_t ro = ((uint32_t)u * G + k0) * 8u + (uint32_t)pq * 8u;
+        const uint32_t rr = ((uint32_t)ur * G + k0) * 8u;
+        F::store_output(v, [&](int c, int, float2 x) {
+            gb.store_if((nf >> (c / P)) & 1u, x, ro + c * 8u);
+            const int cr = (G - pq - c) & (G - 1);
+            gb.store_if(ur != u && ((nr >> (c / P)) & 1u),
+                    make_float2(x.x, -x.y), rr + (uint32_t)cr * 8u);
+        });
+    }
+}
+
 // Row pass (forward) of the real-input form: quads as k_rows_herm; half 0
 // forms X[k] (grid rows k and G - k), half 1 X[G/2 - k] (rows G/2 - k and
 // G/2 + k; for k = 0 the row G/2 alone, for k = G/4 nothing). Only the
@@ -1537,6 +1841,20 @@ bool herm_degrid_enabled(const ImageParams<float>& ip)
     return on && !ip.do_w && ip.G >= 2048 && ip.G <= 8192;
 }
 
+// Row pass of the real-output gridding transform in the single-row form
+// (k_rows_herm1 + k_cols_a_herm_pairs) instead of row quads (env
+// SDP_ES_HERM_ROWS=1; A/B).
+bool herm_rows1()
+{
+    static int on = -1;
+    if (on < 0)
+    {
+        const char* e = getenv("SDP_ES_HERM_ROWS");
+        on = (e && e[0] == '1') ? 1 : 0;
+    }
+    return on != 0;
+}
+
 template<int N1, int N2>
 int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
         const uint32_t* tiles, int ncoarse, uint32_t* occ,
@@ -1559,6 +1877,29 @@ int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
                     ncoarse, G, occ);
             SDP_HIP_CHECK_LAUNCH(&st);
             if (st) return st;
+        }
+        if (herm_rows1())
+        {
+            // One H row per workgroup iteration; Z formed in column pass A.
+            const size_t lds = row_lds_bytes(G);
+            SDP_HIP_CHECK((allow_lds<k_rows_herm1<G>>(lds)), &st);
+            if (st) return st;
+            const int blocks = std::min(G / 2 + 1, num_cus() *
+                    (int)std::max<size_t>(1, (160 * 1024) / lds));
+            k_rows_herm1<G><<<blocks, RowPlan<G>::P, lds, stream>>>(
+                    grid, g.k0, g.M, W, tiles ? occ : nullptr);
+            SDP_HIP_CHECK_LAUNCH(&st);
+            if (st) return st;
+            constexpr size_t cl = cols_pair_lds_bytes<HS::N2>();
+            SDP_HIP_CHECK((allow_lds<k_cols_a_herm_pairs<HS::N1, HS::N2>>(cl)),
+                    &st);
+            if (st) return st;
+            const dim3 cg = col_grid<k_cols_a_herm_pairs<HS::N1, HS::N2>>(
+                    HS::N1 / 2 + 1, g.M, ColPlan<HS::N2>::B);
+            k_cols_a_herm_pairs<HS::N1, HS::N2><<<cg, 256, cl, stream>>>(
+                    grid, g.M, W);
+            SDP_HIP_CHECK_LAUNCH(&st);
+            return st;
         }
         const size_t lds = 2 * row_lds_bytes(G);
         SDP_HIP_CHECK((allow_lds<k_rows_herm<G>>(lds)), &st);
@@ -1640,6 +1981,25 @@ int image_to_grid_herm(const Geometry& g, const float2* W, float2* grid,
                     ncoarse, G, need);
             SDP_HIP_CHECK_LAUNCH(&st);
             if (st) return st;
+        }
+        if (herm_rows1())
+        {
+            // X formed in column pass B; one row per workgroup iteration.
+            const dim3 cg = col_grid<k_cols_b_image_herm_pairs<HS::N1,
+                    HS::N2>>(HS::N2 / 2 + 1, g.M, ColPlan<HS::N1>::B);
+            k_cols_b_image_herm_pairs<HS::N1, HS::N2><<<cg, 256,
+                    kColLdsBytes, stream>>>(grid, g.M, W);
+            SDP_HIP_CHECK_LAUNCH(&st);
+            if (st) return st;
+            const size_t lds = row_lds_bytes(G);
+            SDP_HIP_CHECK((allow_lds<k_rows_image_herm1<G>>(lds)), &st);
+            if (st) return st;
+            const int blocks = std::min(G / 2 + 1, num_cus() *
+                    (int)std::max<size_t>(1, (160 * 1024) / lds));
+            k_rows_image_herm1<G><<<blocks, RowPlan<G>::P, lds, stream>>>(
+                    grid, g.k0, g.M, W, tiles ? need : nullptr);
+            SDP_HIP_CHECK_LAUNCH(&st);
+            return st;
         }
         k_cols_b_image_herm<HS::N1, HS::N2><<<col_grid<k_cols_b_image_herm<
                 HS::N1, HS::N2>>(HS::N2, g.M, ColPlan<HS::N1>::B), 256,

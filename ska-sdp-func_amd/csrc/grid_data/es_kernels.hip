@@ -1585,7 +1585,8 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         int sub[4], rank[4];
         pool_count<kSub>(s_pc, lane, wave, wlo_r, whi_r, wlo_c, whi_c, sub,
                 rank);
-        __syncthreads();   // B1: previous chunk consumed
+        lds_barrier();   // B1: previous chunk consumed (LDS only: the
+                         // next records stay in flight)
         if (on_plane)
         {
 #pragma clang fp contract(off)
@@ -1603,37 +1604,86 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         }
         s_acc_re[t] = 0.0f;
         s_acc_im[t] = 0.0f;
-        __syncthreads();   // B2: counts, tables, accumulators ready
+        lds_barrier();   // B2: counts, tables, accumulators ready
         int beg_l, tot_l, base_l;
         pool_layout<kSub * kSub>(s_pc, lane, wave, beg_l, tot_l, base_l);
+        // Visit groups of 16 (one sub-tile each, sub-tile-major). The
+        // chunk's groups are split evenly over the four waves in contiguous
+        // ranges: with sorted records the visits crowd into the few
+        // sub-tiles the chunk's entries start in, so a fixed sub-tile per
+        // wave would leave waves idle at the next barrier. Lane L < 25
+        // holds sub-tile L's group count and inclusive group end.
+        constexpr int kNS = kSub * kSub;
+        const int ng_l = lane < kNS ? (tot_l + 15) >> 4 : 0;
+        int gend_l = ng_l;
+#pragma unroll
+        for (int d = 1; d < 32; d *= 2)
+        {
+            const int y = __shfl_up(gend_l, d, 64);
+            if (lane >= d) gend_l += y;
+        }
+        const int n_groups = __builtin_amdgcn_readlane(gend_l, kNS - 1);
+        const int g0 = (n_groups * wave) >> 2;
+        const int g1 = (n_groups * (wave + 1)) >> 2;
+        // Sub-tile of group g: the number of sub-tiles whose groups end at
+        // or before g (empty sub-tiles end where their predecessor does).
+        auto st_of = [&](int g) -> int {
+            return (int)__popcll(__ballot(lane < kNS && gend_l <= g));
+        };
+        auto st_after = [&](int st) -> int {
+            const int ge = __builtin_amdgcn_readlane(gend_l, st);
+            return ge < g1 ? st_of(ge) : kNS;
+        };
+        // A operands straight from the grid (L2 / HBM):
+        // G[r0 + R0 + jl][c0 + C0 + 4 kk + kq], kk = 0..3; the next
+        // sub-tile's are in flight while the current one's visits run.
+        auto load_a = [&](int st, float2 (&v)[4]) {
+            const int R0 = (st / kSub) * 16, C0 = (st % kSub) * 16;
+            const int grow = r0 + R0 + jl;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+            {
+                const int gcol = c0 + C0 + 4 * kk + kq;
+                v[kk] = make_float2(0.0f, 0.0f);
+                if (st < kNS && grow < p.G && gcol < p.G)
+                    v[kk] = g2[(size_t)grow * p.G + gcol];
+            }
+        };
+        int st_cur = g0 < g1 ? st_of(g0) : kNS;
+        int st_nxt = st_cur < kNS ? st_after(st_cur) : kNS;
+        float2 a_cur[4], a_nxt[4];
+        load_a(st_cur, a_cur);
+        load_a(st_nxt, a_nxt);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
         {
             const int pos = __shfl(base_l, max(sub[k], 0), 64) + rank[k];
             if (sub[k] >= 0) s_pool[pos] = pk;
         }
-        __syncthreads();   // B3: pool complete
-        for (int st = wave; st < kSub * kSub; st += 4)
+        lds_barrier();   // B3: pool complete (the A loads stay in flight)
+        int gg = g0;
+        while (st_cur < kNS)
         {
-            const int sts = __builtin_amdgcn_readfirstlane(st);
+            const int sts = __builtin_amdgcn_readfirstlane(st_cur);
             const int cnt = __builtin_amdgcn_readlane(tot_l, sts);
-            if (cnt == 0) continue;
             const int v_beg = __builtin_amdgcn_readlane(beg_l, sts);
+            const int ge = __builtin_amdgcn_readlane(gend_l, sts);
+            const int gb = ge - __builtin_amdgcn_readlane(ng_l, sts);
             const int R0 = (sts / kSub) * 16, C0 = (sts % kSub) * 16;
-            // A operands straight from the grid (L2 / HBM):
-            // G[r0 + R0 + jl][c0 + C0 + 4 kk + kq], kk = 0..3.
             float a_re[4], a_im[4];
-            const int grow = r0 + R0 + jl;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk)
             {
-                const int gcol = c0 + C0 + 4 * kk + kq;
-                float2 v = make_float2(0.0f, 0.0f);
-                if (grow < p.G && gcol < p.G) v = g2[(size_t)grow * p.G + gcol];
-                a_re[kk] = v.x;
-                a_im[kk] = v.y;
+                a_re[kk] = a_cur[kk].x;
+                a_im[kk] = a_cur[kk].y;
+                a_cur[kk] = a_nxt[kk];
             }
-            for (int g = 0; g < cnt; g += 16)
+            const int g_lo = (gg - gb) * 16, g_hi = (min(ge, g1) - gb) * 16;
+            gg = ge;
+            st_cur = st_nxt;
+            st_nxt = st_cur < kNS ? st_after(st_cur) : kNS;
+            load_a(st_nxt, a_nxt);
+            for (int g = g_lo; g < g_hi; g += 16)
             {
 #pragma clang fp contract(off)
                 const bool valid = g + jl < cnt;
@@ -1680,7 +1730,7 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
                 }
             }
         }
-        __syncthreads();
+        lds_barrier();
         if (on_plane)
         {
             const uint64_t idx = (uint64_t)__float_as_uint(r.w);
