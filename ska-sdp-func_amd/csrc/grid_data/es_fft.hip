@@ -935,20 +935,20 @@ k_rows_herm1(float2* __restrict__ grid, int k0, int M,
 // Column pass A of the half-length transform on the Bh rows of
 // k_rows_herm1: it first forms the Z rows, Z[m] = (Bh[m] + conj Bh[G/2 - m])
 // + i (Bh[m] - conj Bh[G/2 - m]) e^{2 pi i m / G}, then runs k_cols_a_herm's
-// length-N2 transforms. Rows m = u1 + N1 n2 (class u1) pair with rows of
-// class N1 - u1 (element N2 - 1 - n2), so workgroup j takes the classes j
-// and N1 - j together (j = 0: class 0 alone, whose element n2 pairs with
-// N2 - n2 and element 0 with Bh[G/2]; j = N1/2: class N1/2 alone); the
-// partner values are exchanged through LDS.
-template<int N2>
-constexpr size_t cols_pair_lds_bytes()
-{
-    return std::max(kColLdsBytes,
-            (size_t)(N2 + 1) * ColPlan<N2>::B * sizeof(float2));
-}
-
+// length-N2 transforms. Rows m = u1 + N1 n2 (class u1) pair with element
+// N2 - 1 - n2 of class N1 - u1, so workgroup j takes the classes j and
+// N1 - j. Thread p holds elements n2 = p + PT r of class j and, loaded as
+// thread p' = PT - 1 - p would, the mirrored elements N2 - 1 - n2 of class
+// N1 - j: every pair meets in one thread's registers (no exchange), and
+// the thread then transforms class N1 - j in the role of thread p' (slot
+// 15 - r). Workgroup 0 (class 0: element n2 pairs with N2 - n2, element 0
+// with Bh[G/2]) and workgroup N1/2 (class N1/2 with itself) load their
+// partners a second time and transform one class.
+#ifndef SDP_PAIRS_WAVES
+#define SDP_PAIRS_WAVES 2
+#endif
 template<int N1, int N2>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_COLA_WAVES)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_PAIRS_WAVES)))
 k_cols_a_herm_pairs(float2* __restrict__ grid, int M,
         const float2* __restrict__ W)
 {
@@ -957,82 +957,75 @@ k_cols_a_herm_pairs(float2* __restrict__ grid, int M,
     static_assert(F::EPT == 16 && PT * 16 == N2, "element n2 = p + PT r");
     extern __shared__ float2 lds[];
     const int c = threadIdx.x % B, p = threadIdx.x / B;
-    const int ja = blockIdx.x, jb = (N1 - ja) & (N1 - 1);
-    const bool pair = ja != jb;
+    const int ja = blockIdx.x, jb = N1 - ja;      // ja = 0: jb unused
+    const bool pair = ja != 0 && 2 * ja != N1;
     const Buf gb(grid, grid_bytes(G, 0));
     F f;
-    f.init(p, W, G);
     const int ncb = (M + B - 1) / B;
     constexpr uint32_t kStep = (uint32_t)N1 * G * 8u;   // one n2 / k2 step
-    const uint32_t so_a = (uint32_t)ja * G * 8u, so_b = (uint32_t)jb * G * 8u;
-    // Z of class u1 from its own Bh values v and the partners' from LDS
-    // (rows n2' of the class the LDS holds).
-    auto form_z = [&](float2 (&v)[16], int u1, bool self0, int cq) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-        {
-            const int n2 = p + PT * r;
-            const int n2p = self0 ? N2 - n2 : N2 - 1 - n2;
-            const float2 b = lds[n2p * B + cq];
-            const float2 a = v[r];
-            const float2 wt = W[u1 + N1 * n2];
-            const float2 w = make_float2(wt.x, -wt.y);    // e^{2 pi i m / G}
-            const float2 xe = make_float2(a.x + b.x, a.y - b.y);
-            const float2 xo = cmul(make_float2(a.x - b.x, a.y + b.y), w);
-            v[r] = make_float2(xe.x - xo.y, xe.y + xo.x);
-        }
-    };
-    auto to_lds = [&](const float2 (&v)[16], int cq) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) lds[(p + PT * r) * B + cq] = v[r];
-    };
+    const uint32_t so_a = (uint32_t)ja * G * 8u;
+    const uint32_t so_b = (uint32_t)(jb & (N1 - 1)) * G * 8u;
     for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
     {
         const int pq = opaque(p), cq = opaque(c);
+        const int pm = PT - 1 - pq;                   // mirror thread
         const int col = cb * B + cq;
         const bool ok = col < M;
-        const uint32_t vo = ((uint32_t)pq * N1 * G + col) * 8u;
-        float2 va[16], vb[16];
-        F::load_input(va, [&](int e) {
-            return ok ? gb.load(vo, so_a + e * kStep) : make_float2(0.f, 0.f);
-        });
-        if (pair)
-            F::load_input(vb, [&](int e) {
-                return ok ? gb.load(vo, so_b + e * kStep)
-                          : make_float2(0.f, 0.f);
-            });
-        // Class 0's element 0 pairs with Bh[G/2] (row N1 N2).
-        float2 xrow = make_float2(0.f, 0.f);
-        if (ja == 0 && p == 0 && ok)
-            xrow = gb.load(((uint32_t)N1 * N2 * G + col) * 8u, 0);
-        __syncthreads();                 // previous transform's LDS use done
-        if (pair) to_lds(vb, cq);
-        else to_lds(va, cq);
-        if (ja == 0 && p == 0) lds[N2 * B + cq] = xrow;
-        __syncthreads();
-        float2 za[16];
+        float2 za[16], zb[16];
+        // Own elements of class ja; partners: class 0 element N2 - n2
+        // (row N1 (N2 - n2); n2 = 0 -> row G/2), else element N2 - 1 - n2
+        // of class jb (class ja itself for ja = N1/2).
 #pragma unroll
-        for (int r = 0; r < 16; ++r) za[r] = va[r];
-        form_z(za, ja, ja == 0, cq);
-        if (pair)
+        for (int r = 0; r < 16; ++r)
         {
-            __syncthreads();
-            to_lds(va, cq);
-            __syncthreads();
-            form_z(vb, jb, false, cq);
+            const int n2 = pq + PT * r;
+            const uint32_t co = (uint32_t)col * 8u;
+            za[r] = ok ? gb.load(co + (uint32_t)n2 * kStep, so_a)
+                       : make_float2(0.f, 0.f);
+            const int n2p = ja == 0 ? N2 - n2 : N2 - 1 - n2;
+            zb[r] = ok ? gb.load(co + (uint32_t)n2p * kStep,
+                    ja == 0 ? 0u : so_b) : make_float2(0.f, 0.f);
         }
-        __syncthreads();                 // partners read: LDS free
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+        {
+            const int n2 = pq + PT * r;
+            const int n2p = ja == 0 ? N2 - n2 : N2 - 1 - n2;
+            const float2 a = za[r], b = zb[r];
+            const float2 wa = W[ja + N1 * n2];            // conj: e^{+}
+            const float2 xa = make_float2(a.x + b.x, a.y - b.y);
+            const float2 ya = cmul(make_float2(a.x - b.x, a.y + b.y),
+                    make_float2(wa.x, -wa.y));
+            za[r] = make_float2(xa.x - ya.y, xa.y + ya.x);
+            if (pair)
+            {
+                const float2 wb = W[jb + N1 * n2p];
+                const float2 xb = make_float2(b.x + a.x, b.y - a.y);
+                const float2 yb = cmul(make_float2(b.x - a.x, b.y + a.y),
+                        make_float2(wb.x, -wb.y));
+                zb[r] = make_float2(xb.x - yb.y, xb.y + yb.x);
+            }
+        }
+        f.init(pq, W, G);
         f.transform(za, pq, lds, ColIdx<B>{cq});
+        const uint32_t vo = ((uint32_t)pq * N1 * G + col) * 8u;
         F::store_output(za, [&](int e, int i, float2 x) {
             const float2 fs = F::twiddle(W, 2 * ja * F::out_index(pq, i));
             if (ok) gb.store(cmul(x, fs), vo, so_a + e * kStep);
         });
         if (pair)
         {
-            f.transform(vb, pq, lds, ColIdx<B>{cq});
-            F::store_output(vb, [&](int e, int i, float2 x) {
-                const float2 fs = F::twiddle(W, 2 * jb * F::out_index(pq, i));
-                if (ok) gb.store(cmul(x, fs), vo, so_b + e * kStep);
+            // Class jb in the role of the mirror thread: its slot r' holds
+            // element pm + PT r', i.e. this thread's slot 15 - r'.
+            float2 v[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] = zb[15 - r];
+            f.init(pm, W, G);
+            f.transform(v, pm, lds, ColIdx<B>{cq});
+            const uint32_t vb = ((uint32_t)pm * N1 * G + col) * 8u;
+            F::store_output(v, [&](int e, int i, float2 x) {
+                const float2 fs = F::twiddle(W, 2 * jb * F::out_index(pm, i));
+                if (ok) gb.store(cmul(x, fs), vb, so_b + e * kStep);
             });
         }
     }
@@ -1489,96 +1482,103 @@ k_cols_b_image_herm(float2* __restrict__ grid, int M,
 // Z[G/2 - k]) e^{-2 pi i k / G} / 2 itself and writes X[k] into row k
 // (k in [0, G/2]; X[G/2] from Z[0]), so the row pass takes one row per
 // workgroup iteration (k_rows_image_herm1). Z rows k = k2 + N2 k1 of class
-// k2 pair with class N2 - k2 (element N1 - 1 - k1); workgroup j takes the
-// classes j and N2 - j (j = 0: class 0 alone, element k1 paired with
-// N1 - k1 mod N1; j = N2/2 alone); partners are exchanged through LDS.
+// k2 pair with element N1 - 1 - k1 of class N2 - k2: workgroup j takes the
+// classes j and N2 - j, transforming the second in the role of the mirror
+// thread p' = PT - 1 - p, whose output slot 15 - i holds exactly the
+// partner of this thread's slot i (out_index(p', 15 - i) = N1 - 1 -
+// out_index(p, i)); the pairs meet in registers. Workgroup N2/2 (class
+// N2/2 with itself) transforms its class twice; workgroup 0 (class 0,
+// element k1 paired with N1 - k1 mod N1) exchanges through LDS.
+#ifndef SDP_PAIRS_WAVES
+#define SDP_PAIRS_WAVES 2
+#endif
 template<int N1, int N2>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_PAIRS_WAVES)))
 k_cols_b_image_herm_pairs(float2* __restrict__ grid, int M,
         const float2* __restrict__ W)
 {
-    constexpr int G = 2 * N1 * N2, B = ColPlan<N1>::B;
+    constexpr int G = 2 * N1 * N2, B = ColPlan<N1>::B, PT = ColPlan<N1>::P;
     using F = ColFft<N1, -1>;
     static_assert(F::EPT == 16 && (size_t)N1 * B * sizeof(float2) <=
-            kColLdsBytes, "partner exchange fits the transform's LDS");
+            kColLdsBytes, "class-0 exchange fits the transform's LDS");
+    static_assert(F::out_const(15) + F::out_const(0) == N1 - PT &&
+            F::out_const(14) + F::out_const(1) == N1 - PT &&
+            F::out_const(9) + F::out_const(6) == N1 - PT,
+            "mirror slot 15 - i holds element N1 - 1 - k1");
     extern __shared__ float2 lds[];
     const int c = threadIdx.x % B, p = threadIdx.x / B;
-    const int ja = blockIdx.x, jb = (N2 - ja) & (N2 - 1);
-    const bool pair = ja != jb;
+    const int ja = blockIdx.x, jb = N2 - ja;
+    const bool two = ja != 0;                    // second transform
+    const bool pair = two && 2 * ja != N2;       // second class stored
     const Buf gb(grid, grid_bytes(G, 0));
     F f;
-    f.init(p, W, G);
     const int ncb = (M + B - 1) / B;
     constexpr uint32_t kStep = (uint32_t)N2 * G * 8u;
-    const uint32_t so_a = (uint32_t)ja * G * 8u, so_b = (uint32_t)jb * G * 8u;
-    auto to_lds = [&](const float2 (&v)[16], int pq, int cq) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) lds[F::out_index(pq, i) * B + cq] = v[i];
-    };
-    // X of class k2 from its own Z values and the partners' in LDS.
-    auto form_x = [&](float2 (&v)[16], int k2, bool self0, int pq, int cq) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-        {
-            const int k1 = F::out_index(pq, i);
-            const int k1p = self0 ? (N1 - k1) & (N1 - 1) : N1 - 1 - k1;
-            const float2 a = v[i], b = lds[k1p * B + cq];
-            const float2 w = W[k2 + N2 * k1];            // e^{-2 pi i k / G}
-            const float2 dw = cmul(make_float2(a.x - b.x, a.y + b.y), w);
-            v[i] = make_float2(0.5f * ((a.x + b.x) + dw.y),
-                    0.5f * ((a.y - b.y) - dw.x));
-        }
+    const uint32_t so_a = (uint32_t)ja * G * 8u;
+    const uint32_t so_b = (uint32_t)(jb & (N2 - 1)) * G * 8u;
+    auto mix = [](float2 a, float2 b, float2 w) {
+        const float2 dw = cmul(make_float2(a.x - b.x, a.y + b.y), w);
+        return make_float2(0.5f * ((a.x + b.x) + dw.y),
+                0.5f * ((a.y - b.y) - dw.x));
     };
     for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
     {
         const int pq = opaque(p), cq = opaque(c);
+        const int pm = PT - 1 - pq;
         const int col = cb * B + cq;
         const bool ok = col < M;
         const uint32_t vo = ((uint32_t)pq * N2 * G + col) * 8u;
+        const uint32_t vm = ((uint32_t)pm * N2 * G + col) * 8u;
         float2 va[16], vb[16];
         F::load_input(va, [&](int e) {
             return ok ? gb.load(vo, so_a + e * kStep) : make_float2(0.f, 0.f);
         });
-        if (pair)
+        if (two)
             F::load_input(vb, [&](int e) {
-                return ok ? gb.load(vo, so_b + e * kStep)
+                return ok ? gb.load(vm, so_b + e * kStep)
                           : make_float2(0.f, 0.f);
             });
+        f.init(pq, W, G);
         f.transform(va, pq, lds, ColIdx<B>{cq});
-        if (pair) f.transform(vb, pq, lds, ColIdx<B>{cq});
-        __syncthreads();                 // transforms' LDS use done
-        to_lds(pair ? vb : va, pq, cq);
-        __syncthreads();
-        // Z[0] (class 0, element 0) also gives X[G/2] (partner Z[0],
-        // e^{-i pi} = -1), written into row G/2.
-        float2 z0 = va[0];
-        float2 xa[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) xa[i] = va[i];
-        form_x(xa, ja, ja == 0, pq, cq);
-        if (pair)
+        if (two)
         {
-            __syncthreads();
-            to_lds(va, pq, cq);
-            __syncthreads();
-            form_x(vb, jb, false, pq, cq);
+            f.init(pm, W, G);
+            f.transform(vb, pm, lds, ColIdx<B>{cq});
         }
-        const uint32_t vs = ((uint32_t)pq * N2 * G + col) * 8u;
-        F::store_output(xa, [&](int e, int, float2 x) {
-            if (ok) gb.store(x, vs, so_a + e * kStep);
+        else
+        {
+            // Class 0: partner of k1 is (N1 - k1) mod N1, through LDS.
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                lds[F::out_index(pq, i) * B + cq] = va[i];
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                vb[15 - i] = lds[((N1 - F::out_index(pq, i)) & (N1 - 1)) * B +
+                        cq];
+        }
+        const float2 z0 = va[0];                 // Z[0] for pq == 0, ja == 0
+        // In place: slot i of va and slot 15 - i of vb are read only here.
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+        {
+            const int k1 = F::out_index(pq, i);
+            const float2 a = va[i], b = vb[15 - i];
+            va[i] = mix(a, b, W[ja + N2 * k1]);            // e^{-2 pi i k / G}
+            if (pair)
+                vb[15 - i] = mix(b, a, W[jb + N2 * (N1 - 1 - k1)]);
+        }
+        F::store_output(va, [&](int e, int, float2 x) {
+            if (ok) gb.store(x, vo, so_a + e * kStep);
         });
         if (pair)
             F::store_output(vb, [&](int e, int, float2 x) {
-                if (ok) gb.store(x, vs, so_b + e * kStep);
+                if (ok) gb.store(x, vm, so_b + e * kStep);
             });
-        if (ja == 0 && pq == 0 && ok && F::out_index(0, 0) == 0)
-        {
-            const float2 dw = cmul(make_float2(0.0f, z0.y + z0.y),
-                    make_float2(-1.0f, 0.0f));
-            const float2 x = make_float2(0.5f * ((z0.x + z0.x) + dw.y),
-                    0.5f * (0.0f - dw.x));
-            gb.store(x, ((uint32_t)(G / 2) * G + col) * 8u, 0);
-        }
+        if (ja == 0 && pq == 0 && ok)
+            gb.store(mix(z0, z0, make_float2(-1.0f, 0.0f)),
+                    ((uint32_t)(G / 2) * G + col) * 8u, 0);
     }
 }
 
@@ -1890,14 +1890,10 @@ int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
                     grid, g.k0, g.M, W, tiles ? occ : nullptr);
             SDP_HIP_CHECK_LAUNCH(&st);
             if (st) return st;
-            constexpr size_t cl = cols_pair_lds_bytes<HS::N2>();
-            SDP_HIP_CHECK((allow_lds<k_cols_a_herm_pairs<HS::N1, HS::N2>>(cl)),
-                    &st);
-            if (st) return st;
             const dim3 cg = col_grid<k_cols_a_herm_pairs<HS::N1, HS::N2>>(
                     HS::N1 / 2 + 1, g.M, ColPlan<HS::N2>::B);
-            k_cols_a_herm_pairs<HS::N1, HS::N2><<<cg, 256, cl, stream>>>(
-                    grid, g.M, W);
+            k_cols_a_herm_pairs<HS::N1, HS::N2><<<cg, 256, kColLdsBytes,
+                    stream>>>(grid, g.M, W);
             SDP_HIP_CHECK_LAUNCH(&st);
             return st;
         }

@@ -1515,6 +1515,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
 // evaluated once at staging into LDS tables; visits are packed {entry,
 // u0 - tile row, v0 - tile col} words; the pool is laid out without atomics
 // and the next chunk's records are prefetched.
+#ifndef SDP_GATHER_BALANCE
+#define SDP_GATHER_BALANCE 1
+#endif
 template<bool DO_W, int NTAP>
 __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
@@ -1630,10 +1633,22 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         auto st_of = [&](int g) -> int {
             return (int)__popcll(__ballot(lane < kNS && gend_l <= g));
         };
+#if SDP_GATHER_BALANCE
         auto st_after = [&](int st) -> int {
             const int ge = __builtin_amdgcn_readlane(gend_l, st);
             return ge < g1 ? st_of(ge) : kNS;
         };
+        const int st_first = g0 < g1 ? st_of(g0) : kNS;
+#else
+        // (A/B: sub-tiles st = wave (mod 4) per wave, whole.)
+        auto next_fixed = [&](int st) -> int {
+            for (; st < kNS; st += 4)
+                if (__builtin_amdgcn_readlane(ng_l, st) != 0) break;
+            return st;
+        };
+        auto st_after = [&](int st) -> int { return next_fixed(st + 4); };
+        const int st_first = next_fixed(wave);
+#endif
         // A operands straight from the grid (L2 / HBM):
         // G[r0 + R0 + jl][c0 + C0 + 4 kk + kq], kk = 0..3; the next
         // sub-tile's are in flight while the current one's visits run.
@@ -1649,7 +1664,7 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
                     v[kk] = g2[(size_t)grow * p.G + gcol];
             }
         };
-        int st_cur = g0 < g1 ? st_of(g0) : kNS;
+        int st_cur = st_first;
         int st_nxt = st_cur < kNS ? st_after(st_cur) : kNS;
         float2 a_cur[4], a_nxt[4];
         load_a(st_cur, a_cur);
@@ -1678,7 +1693,11 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
                 a_im[kk] = a_cur[kk].y;
                 a_cur[kk] = a_nxt[kk];
             }
+#if SDP_GATHER_BALANCE
             const int g_lo = (gg - gb) * 16, g_hi = (min(ge, g1) - gb) * 16;
+#else
+            const int g_lo = 0, g_hi = (ge - gb) * 16;
+#endif
             gg = ge;
             st_cur = st_nxt;
             st_nxt = st_cur < kNS ? st_after(st_cur) : kNS;
