@@ -2,13 +2,15 @@
 # Round-4 A/B: correctness of the variants under test (short pytest
 # subsets), then kernel traces of each (scripts/kt_variants.sh) with the
 # per-kernel averages printed.  scripts/gpu_r4_ab.sh OUT "name:dir[:VAR=v] ..."
-#   PRE: optional list of "dir:VAR=v:pytest-k" correctness runs.
+#   PRE: optional list of "dir:VAR=v:pytest-k" correctness runs ('+' in
+#   the -k expression stands for a space).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=$1; AB=$2
 mkdir -p "$OUT"
 for spec in $PRE; do
     IFS=: read -r d e k <<< "$spec"
+    k=${k//+/ }                      # '+' stands for a space in -k
     env SKA_SDP_FUNC_LIB_DIR="$d" $e timeout -k 10 300 python -u -m pytest \
         tests -m gpu -x -q --timeout 200 --timeout-method thread -k "$k" \
         > "$OUT/pre_$(basename "$d").log" 2>&1 \

@@ -6,6 +6,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include <hip/hip_runtime.h>
 
@@ -26,9 +27,16 @@ __device__ __forceinline__ T conv_corr_n(const ImageParams<T>& ip, T k)
     T c = T(0);
     for (uint32_t i = 0; i < np; ++i)
     {
-        c = (T)((double)c + (double)ip.quad_kernel[i] *
-                cos(kPi * (double)k * (double)support *
-                (double)ip.quad_nodes[i]) * (double)ip.quad_weights[i]);
+        // The argument in double as the reference forms it; in a float
+        // plan its cosine in float (the term is rounded to float anyway):
+        // ~1e-7 relative instead of the double libm cosine, at a fraction
+        // of the FP64 cost (14 terms per pixel of the 3-D correction).
+        const double arg = kPi * (double)k * (double)support *
+                (double)ip.quad_nodes[i];
+        const double cs = std::is_same<T, float>::value ?
+                (double)cosf((float)arg) : cos(arg);
+        c = (T)((double)c + (double)ip.quad_kernel[i] * cs *
+                (double)ip.quad_weights[i]);
     }
     return c * support;
 }

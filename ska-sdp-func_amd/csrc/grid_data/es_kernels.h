@@ -28,6 +28,9 @@ constexpr int kCoarseTile = kTile * kCoarse;   // 256 cells
 constexpr int kBinsPerPass = 16384;    // LDS histogram capacity (64 KiB)
 constexpr int kPiece = 4096;           // max entries per scatter work item
 constexpr int kMaxChunks = 1024;       // chunks of visibilities per bucketing
+constexpr int kCountChunks = 4;        // chunks per counting workgroup
+constexpr int kGroupChunks = 16;       // chunks per level-2 group (and per
+                                       // row of the tile count table)
 constexpr int kMaxSuperBins = 1024;    // super bins (first bucketing level)
 constexpr int kMaxSuperTiles = 4096;   // tiles per super bin (S^2, S <= 64)
 constexpr int kTapPolyPairs = 3;       // interior taps 1..6 of W = 8
@@ -73,7 +76,9 @@ void es_tap_poly_fit(double beta_f32, float out[kTapPolyPairs]
 // Scratch owned by a plan (device pointers).
 struct BucketScratch
 {
-    uint32_t* table = nullptr;      // [num_chunks][tstride] counts / offsets
+    uint32_t* table = nullptr;      // [chunks][nsbins] super-bin counts /
+                                    // offsets, then [groups][nbins] tile
+                                    // counts / offsets (bucket_table_entries)
     uint32_t* bin_count = nullptr;  // [tstride]: tile then super-bin totals
     uint32_t* bin_start = nullptr;  // [nbins + 1]
     uint32_t* item_start = nullptr; // [nbins + 1]
@@ -91,6 +96,9 @@ struct BucketScratch
 // table row length (the chunk-by-bin table stays below 2^31 bytes, the
 // range of the buffer addressing in k_scan_columns).
 int num_chunks(int64_t num_vis, int tstride);
+
+// Entries of BucketScratch::table for nc chunks.
+size_t bucket_table_entries(int nc, int nbins, int nsbins);
 
 // Super-bin geometry for ntiles tiles per axis: sets sshift, nsuper, nsbins
 // (the smallest S = 2^sshift >= 8 with ceil(ntiles / S)^2 <= kMaxSuperBins).

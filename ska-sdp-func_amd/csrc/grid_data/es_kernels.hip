@@ -268,52 +268,79 @@ __device__ __forceinline__ void tile_span(const EsParams<T>& p, int u0, int u1,
     tv1 = MODE == MODE_GRID ? (v1 + half) / kTile : tv0;
 }
 
+// Counting pass. A workgroup takes kCountChunks consecutive chunks of rows:
+// per chunk it counts the records of every super bin (first level, one per
+// visibility and super bin its tiles touch) into the chunk's row of the
+// super table [chunks][nsbins], and over all its chunks the records of every
+// tile into an LDS histogram that is added (global atomics, nonzero bins)
+// to its chunk group's row of the group table [groups][nbins] (kGroupChunks
+// chunks per group, the granularity k_bucket_fill2 needs). Round 3 wrote a
+// [chunks][tiles + super bins] table (68 MB at config 2), read and
+// rewritten by the column scan: ~200 MB of bookkeeping per bucketing.
 template<typename T, int MODE, int NT>
 __global__ __launch_bounds__(NT) void k_bucket_count(EsParams<T> p,
-        int64_t num_rows, int num_chan, int64_t chunk, const T* __restrict__ uvw,
-        const T* __restrict__ freq, uint32_t* __restrict__ table)
+        int64_t num_rows, int num_chan, int64_t chunk, int nc,
+        const T* __restrict__ uvw, const T* __restrict__ freq,
+        uint32_t* __restrict__ stable, uint32_t* __restrict__ gtable)
 {
     __shared__ uint32_t hist[kBinsPerPass];
-    __shared__ uint32_t shist[kMaxSuperBins];
+    __shared__ uint32_t shist[kCountChunks][kMaxSuperBins];
     const int pass_base = blockIdx.y * kBinsPerPass;
     const int nb = min(kBinsPerPass, p.nbins - pass_base);
-    // Pass 0 also counts records per super bin (one per visibility and
-    // super bin its tiles touch: the first level of k_bucket_fill1).
     const bool supers = blockIdx.y == 0;
     for (int i = threadIdx.x; i < nb; i += NT) hist[i] = 0;
-    for (int i = threadIdx.x; i < p.nsbins; i += NT) shist[i] = 0;
+    if (supers)
+        for (int i = threadIdx.x; i < kCountChunks * kMaxSuperBins; i += NT)
+            (&shist[0][0])[i] = 0;
     __syncthreads();
     // Chunks are ranges of rows; a thread takes a row and its channels
     // (no 64-bit division per visibility, uvw read once per row).
-    const int64_t r0 = (int64_t)blockIdx.x * chunk;
-    const int64_t r1 = min(num_rows, r0 + chunk);
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += NT)
+    const int c_first = blockIdx.x * kCountChunks;
+#pragma unroll 1
+    for (int q = 0; q < kCountChunks; ++q)
     {
-        const T u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2];
-        for (int c = 0; c < num_chan; ++c)
+        const int64_t r0 = (int64_t)(c_first + q) * chunk;
+        const int64_t r1 = min(num_rows, r0 + chunk);
+        uint32_t* sh = shist[q];
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += NT)
         {
-            Footprint<T> f;
-            if (!footprint(p, u, v, w, freq[c], f)) continue;
-            int tu0, tu1, tv0, tv1;
-            tile_span<T, MODE>(p, f.u0, f.u1, f.v0, f.v1, tu0, tu1, tv0, tv1);
-            for (int tu = tu0; tu <= tu1; ++tu)
-                for (int tv = tv0; tv <= tv1; ++tv)
-                {
-                    const int b = fine_bin(p, tu, tv) - pass_base;
-                    if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
-                }
-            if (supers)
-                for (int su = tu0 >> p.sshift; su <= tu1 >> p.sshift; ++su)
-                    for (int sv = tv0 >> p.sshift; sv <= tv1 >> p.sshift; ++sv)
-                        atomicAdd(&shist[su * p.nsuper + sv], 1u);
+            const T u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2];
+            for (int c = 0; c < num_chan; ++c)
+            {
+                Footprint<T> f;
+                if (!footprint(p, u, v, w, freq[c], f)) continue;
+                int tu0, tu1, tv0, tv1;
+                tile_span<T, MODE>(p, f.u0, f.u1, f.v0, f.v1, tu0, tu1, tv0,
+                        tv1);
+                for (int tu = tu0; tu <= tu1; ++tu)
+                    for (int tv = tv0; tv <= tv1; ++tv)
+                    {
+                        const int b = fine_bin(p, tu, tv) - pass_base;
+                        if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
+                    }
+                if (supers)
+                    for (int su = tu0 >> p.sshift; su <= tu1 >> p.sshift; ++su)
+                        for (int sv = tv0 >> p.sshift; sv <= tv1 >> p.sshift;
+                                ++sv)
+                            atomicAdd(&sh[su * p.nsuper + sv], 1u);
+            }
         }
     }
     __syncthreads();
-    uint32_t* row = table + (size_t)blockIdx.x * p.tstride;
-    for (int i = threadIdx.x; i < nb; i += NT) row[pass_base + i] = hist[i];
+    uint32_t* grow = gtable + (size_t)(c_first / kGroupChunks) * p.nbins +
+            pass_base;
+    for (int i = threadIdx.x; i < nb; i += NT)
+    {
+        const uint32_t n = hist[i];
+        if (n) atomicAdd(&grow[i], n);
+    }
     if (supers)
-        for (int i = threadIdx.x; i < p.nsbins; i += NT)
-            row[p.nbins + i] = shist[i];
+        for (int q = 0; q < kCountChunks && c_first + q < nc; ++q)
+        {
+            uint32_t* row = stable + (size_t)(c_first + q) * p.nsbins;
+            for (int i = threadIdx.x; i < p.nsbins; i += NT)
+                row[i] = shist[q][i];
+        }
 }
 
 // Per bin: exclusive prefix over chunks (in place) and the bin total.
@@ -620,9 +647,6 @@ __device__ __forceinline__ void copy_rec(T* dst, const T* src)
 #ifndef SDP_FILL1_WAVES
 #define SDP_FILL1_WAVES 1   // blocks per CU (VGPR budget 128 / this)
 #endif
-#ifndef SDP_FILL2_GROUPS
-#define SDP_FILL2_GROUPS 64
-#endif
 template<typename T, int W>
 struct Fill1Shape
 {
@@ -644,7 +668,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(
         SDP_FILL1_WAVES * NT / 256))) void k_bucket_fill1(EsParams<T> p,
         int64_t num_rows, int num_chan, int64_t chunk, const T* __restrict__ uvw,
         const T* __restrict__ freq, const T* __restrict__ vis,
-        const T* __restrict__ weight, const uint32_t* __restrict__ table,
+        const T* __restrict__ weight, const uint32_t* __restrict__ stable,
         const uint32_t* __restrict__ bin_count, uint32_t* __restrict__ sb_start,
         T* __restrict__ recs1)
 {
@@ -665,7 +689,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(
     const uint32_t n_sb = block_scan_counts<NT>(bin_count + p.nbins, loff,
             nsb, s_wave);
     __syncthreads();
-    const uint32_t* row = table + (size_t)blockIdx.x * p.tstride + p.nbins;
+    const uint32_t* row = stable + (size_t)blockIdx.x * p.nsbins;
     for (int i = t; i < nsb; i += NT)
     {
         cursor[i] = loff[i] + row[i];
@@ -825,7 +849,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(
 // bytes per tile that the block fills while it stays in L2.
 template<typename T, int MODE, bool DO_W>
 __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
-        int gc, const uint32_t* __restrict__ table,
+        const uint32_t* __restrict__ stable,
+        const uint32_t* __restrict__ gtable,
         const uint32_t* __restrict__ bin_count,
         const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ sb_start, const T* __restrict__ recs1,
@@ -834,9 +859,9 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
     constexpr int kWords = Rec<T, MODE, DO_W>::kWords;
     __shared__ uint32_t cur[kMaxSuperTiles];
     const int t = threadIdx.x, sb = blockIdx.y;
-    const int c0 = blockIdx.x * gc;
+    const int c0 = blockIdx.x * kGroupChunks;
     if (c0 >= nc) return;
-    const int c1 = min(nc, c0 + gc);
+    const int c1 = min(nc, c0 + kGroupChunks);
     const int S = 1 << p.sshift;
     const int su = sb / p.nsuper, sv = sb - su * p.nsuper;
     const int tu_base = su << p.sshift, tv_base = sv << p.sshift;
@@ -846,13 +871,13 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
         if (tu < p.ntiles && tv < p.ntiles)
         {
             const int f = fine_bin(p, tu, tv);
-            cur[j] = bin_start[f] + table[(size_t)c0 * p.tstride + f];
+            cur[j] = bin_start[f] + gtable[(size_t)blockIdx.x * p.nbins + f];
         }
     }
     __syncthreads();
-    const uint32_t* col = table + p.nbins + sb;
-    const uint32_t e0 = sb_start[sb] + col[(size_t)c0 * p.tstride];
-    const uint32_t e1 = c1 < nc ? sb_start[sb] + col[(size_t)c1 * p.tstride] :
+    const uint32_t* col = stable + sb;
+    const uint32_t e0 = sb_start[sb] + col[(size_t)c0 * p.nsbins];
+    const uint32_t e1 = c1 < nc ? sb_start[sb] + col[(size_t)c1 * p.nsbins] :
             sb_start[sb + 1];
     // Four records per thread in flight (loads issued before the LDS
     // atomics and stores of the first).
@@ -1518,12 +1543,28 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
 #ifndef SDP_GATHER_BALANCE
 #define SDP_GATHER_BALANCE 1
 #endif
+#ifndef SDP_GATHER_XCD
+#define SDP_GATHER_XCD 1
+#endif
+// Work item of workgroup w when the real item count n is known on the
+// device (totals[1]): workgroups are dealt to the 8 XCDs round-robin
+// (w mod 8), so XCD x is given the contiguous item range [x q, (x + 1) q),
+// q = ceil(n / 8): spatially adjacent tiles (consecutive bins) then share
+// an XCD's L2 and the halo rows one tile's gather reads of its neighbours
+// are L2 hits. Workgroups past 8 q find no item.
+__device__ __forceinline__ uint32_t xcd_item(uint32_t w, uint32_t n)
+{
+    const uint32_t q = (n + 7) >> 3;
+    const uint32_t x = w & 7u, k = w >> 3;
+    return k < q ? x * q + k : 0xFFFFFFFFu;
+}
+
 template<bool DO_W, int NTAP>
 __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
         const uint32_t* __restrict__ item_bin, const float* __restrict__ grid,
-        float* __restrict__ vis)
+        float* __restrict__ vis, const uint32_t* __restrict__ totals)
 {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     constexpr int kChunk = 256;
@@ -1537,7 +1578,12 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
     __shared__ float s_acc_im[kChunk];
     __shared__ PoolCounts<kSub * kSub> s_pc;
 
+#if SDP_GATHER_XCD
+    const uint32_t item = xcd_item(blockIdx.x, totals[1]);
+    if (item >= totals[1]) return;
+#else
     const uint32_t item = blockIdx.x;
+#endif
     if (item_bin[item] == kNoBin) return;   // past the last work item
     const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
@@ -2039,12 +2085,25 @@ __global__ void k_screen_accumulate(ImageParams<T> ip, int plane,
 template<typename T>
 __global__ void k_apply_correction(ImageParams<T> ip, T* __restrict__ dirty)
 {
+    // The correction depends on |x - h|, |y - h| only: one evaluation per
+    // offset pair (i, j), applied to the up to four pixels h +- i, h +- j
+    // of the image (rows and columns < 2h).
     const int h = ip.N / 2;
-    const int ix = blockIdx.x * blockDim.x + threadIdx.x;
-    const int iy = blockIdx.y * blockDim.y + threadIdx.y;
-    if (ix >= 2 * h || iy >= 2 * h) return;
-    dirty[(size_t)iy * ip.N + ix] *= inv_correction(ip, abs(ix - h),
-            abs(iy - h));
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = blockIdx.y * blockDim.y + threadIdx.y;
+    if (i > h || j > h) return;
+    const T f = inv_correction(ip, i, j);
+    const int xs[2] = {h - i, h + i}, ys[2] = {h - j, h + j};
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+        {
+            const int ix = xs[b], iy = ys[a];
+            if ((a && j == 0) || (b && i == 0) || ix >= 2 * h || iy >= 2 * h)
+                continue;
+            dirty[(size_t)iy * ip.N + ix] *= f;
+        }
 }
 
 // Whole-grid writer for degridding: centre = checker * dirty * phasor.
@@ -2181,6 +2240,12 @@ int num_chunks(int64_t num_vis, int tstride)
             std::min<int64_t>(kMaxChunks, by_table), by_size));
 }
 
+size_t bucket_table_entries(int nc, int nbins, int nsbins)
+{
+    const size_t ng = (size_t)(nc + kGroupChunks - 1) / kGroupChunks;
+    return (size_t)nc * nsbins + ng * nbins;
+}
+
 bool super_geometry(int ntiles, int* sshift, int* nsuper, int* nsbins)
 {
     for (int sh = 3; (1 << (2 * sh)) <= kMaxSuperTiles; ++sh)
@@ -2199,11 +2264,11 @@ bool super_geometry(int ntiles, int* sshift, int* nsuper, int* nsbins)
 
 template<typename T, int MODE, int NT>
 void launch_count(const dim3& g, const EsParams<T>& p, int64_t num_rows,
-        int num_chan, int64_t chunk, const T* uvw, const T* freq,
-        uint32_t* table, hipStream_t stream)
+        int num_chan, int64_t chunk, int nc, const T* uvw, const T* freq,
+        uint32_t* stable, uint32_t* gtable, hipStream_t stream)
 {
     k_bucket_count<T, MODE, NT><<<g, NT, 0, stream>>>(p, num_rows, num_chan,
-            chunk, uvw, freq, table);
+            chunk, nc, uvw, freq, stable, gtable);
 }
 
 // Both record levels: k_bucket_fill1 (chunk blocks) then k_bucket_fill2
@@ -2217,14 +2282,12 @@ void launch_fill(int nc, int64_t chunk, const EsParams<T>& p,
     k_bucket_fill1<T, MODE, DO_W, NT><<<nc, NT, 0, stream>>>(p, num_rows,
             num_chan, chunk, uvw, freq, vis, weight, s->table, s->bin_count,
             s->sb_start, (T*)s->recs1);
-    // SDP_FILL2_GROUPS chunk groups: groups x nsbins blocks, each moving
-    // the records of nc / groups chunks of one super bin.
-    const int groups = std::min(nc, SDP_FILL2_GROUPS);
-    const int gc = (nc + groups - 1) / groups;
-    const int ng = (nc + gc - 1) / gc;
+    // Chunk groups x super bins: each block moves the records of one
+    // group of kGroupChunks chunks of one super bin.
+    const int ng = (nc + kGroupChunks - 1) / kGroupChunks;
     k_bucket_fill2<T, MODE, DO_W><<<dim3(ng, p.nsbins), 256, 0, stream>>>(
-            p, nc, gc, s->table, s->bin_count, s->bin_start, s->sb_start,
-            (const T*)s->recs1, (T*)s->recs);
+            p, nc, s->table, s->table + (size_t)nc * p.nsbins, s->bin_count,
+            s->bin_start, s->sb_start, (const T*)s->recs1, (T*)s->recs);
 }
 
 #define SDP_ES_BY_THREADS(NTV, CALL) \
@@ -2250,26 +2313,39 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
     const int nc = num_chunks(num_vis, p.tstride);
     const int64_t chunk = (num_rows + nc - 1) / nc;   // rows per chunk
     const int passes = (p.nbins + kBinsPerPass - 1) / kBinsPerPass;
-    const dim3 grid_b(nc, passes);
+    const dim3 grid_b((nc + kCountChunks - 1) / kCountChunks, passes);
+    const int ng = (nc + kGroupChunks - 1) / kGroupChunks;
+    uint32_t* stable = s->table;                       // [nc][nsbins]
+    uint32_t* gtable = s->table + (size_t)nc * p.nsbins;   // [ng][nbins]
     const int nt = bucket_threads();
     if (p.nsbins < 1 || p.nsbins > kMaxSuperBins ||
             (1 << (2 * p.sshift)) > kMaxSuperTiles ||
             p.tstride != p.nbins + p.nsbins ||
-            (size_t)nc * p.tstride > s->table_entries)
+            bucket_table_entries(nc, p.nbins, p.nsbins) > s->table_entries)
     {
         SDP_LOG_ERROR("Bucketing geometry / count table mismatch");
         return SDP_ERR_RUNTIME;
     }
+    // The group rows of tile counts are accumulated atomically.
+    SDP_HIP_CHECK(hipMemsetAsync(gtable, 0, (size_t)ng * p.nbins *
+            sizeof(uint32_t), stream), status);
     if (mode == MODE_GRID)
         SDP_ES_BY_THREADS(nt, (launch_count<T, MODE_GRID, NT>(grid_b, p,
-                num_rows, num_chan, chunk, uvw, freq, s->table, stream)))
+                num_rows, num_chan, chunk, nc, uvw, freq, stable, gtable,
+                stream)))
     else
         SDP_ES_BY_THREADS(nt, (launch_count<T, MODE_DEGRID, NT>(grid_b, p,
-                num_rows, num_chan, chunk, uvw, freq, s->table, stream)))
+                num_rows, num_chan, chunk, nc, uvw, freq, stable, gtable,
+                stream)))
     SDP_HIP_CHECK_LAUNCH(status);
-    // Tile and super-bin columns of the count table in one launch.
-    k_scan_columns<<<(p.tstride + 63) / 64, 1024, 0, stream>>>(
-            s->table, nc, p.tstride, s->bin_count);
+    // Column prefixes (in place) and totals: tile counts over the chunk
+    // groups into bin_count[0, nbins), super-bin counts over the chunks
+    // into bin_count[nbins, nbins + nsbins).
+    k_scan_columns<<<(p.nbins + 63) / 64, 1024, 0, stream>>>(
+            gtable, ng, p.nbins, s->bin_count);
+    SDP_HIP_CHECK_LAUNCH(status);
+    k_scan_columns<<<(p.nsbins + 63) / 64, 1024, 0, stream>>>(
+            stable, nc, p.nsbins, s->bin_count + p.nbins);
     SDP_HIP_CHECK_LAUNCH(status);
     k_scan_bins<<<1, 1024, 0, stream>>>(s->bin_count, p.nbins,
             s->bin_start, s->item_start, s->totals, s->item_bin,
@@ -2394,6 +2470,9 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         const float* recs = (const float*)s.recs;
         if (p.support <= 16)
         {
+            // XCD-aware mapping (xcd_item): whole rounds of 8 workgroups,
+            // so that every item of the range split is reached.
+            const uint32_t n_gather = (n_items + 7u) & ~7u;
             if (p.support <= 8 && sort_records && sort_pieces())
             {
                 k_sort_pieces<<<n_items, 256, 0, stream>>>(p,
@@ -2402,17 +2481,21 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
                 SDP_HIP_CHECK_LAUNCH(status);
             }
             if (p.support <= 8 && p.do_w)
-                k_gather_tab<true, 9><<<n_items, 256, 0, stream>>>(p, recs,
-                        s.bin_start, s.item_start, s.item_bin, grid, vis);
+                k_gather_tab<true, 9><<<n_gather, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis,
+                        s.totals);
             else if (p.support <= 8)
-                k_gather_tab<false, 9><<<n_items, 256, 0, stream>>>(p, recs,
-                        s.bin_start, s.item_start, s.item_bin, grid, vis);
+                k_gather_tab<false, 9><<<n_gather, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis,
+                        s.totals);
             else if (p.do_w)
-                k_gather_tab<true, 17><<<n_items, 256, 0, stream>>>(p, recs,
-                        s.bin_start, s.item_start, s.item_bin, grid, vis);
+                k_gather_tab<true, 17><<<n_gather, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis,
+                        s.totals);
             else
-                k_gather_tab<false, 17><<<n_items, 256, 0, stream>>>(p, recs,
-                        s.bin_start, s.item_start, s.item_bin, grid, vis);
+                k_gather_tab<false, 17><<<n_gather, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis,
+                        s.totals);
             SDP_HIP_CHECK_LAUNCH(status);
             return *status;
         }
@@ -2470,8 +2553,8 @@ template<typename T>
 int apply_correction(const ImageParams<T>& ip, T* dirty, hipStream_t stream)
 {
     sdp_Error st = SDP_SUCCESS;
-    k_apply_correction<T><<<image_blocks(ip.N), dim3(64, 4), 0, stream>>>(
-            ip, dirty);
+    k_apply_correction<T><<<image_blocks(ip.N / 2 + 1), dim3(64, 4), 0,
+            stream>>>(ip, dirty);
     SDP_HIP_CHECK_LAUNCH(&st);
     return st;
 }

@@ -267,8 +267,9 @@ void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
         SDP_HIP_CHECK(hipMalloc(&s.recs1, rec_bytes), status);
         s.recs_bytes = *status ? 0 : rec_bytes;
     }
-    const size_t need = (size_t)sdp_es::num_chunks(num_vis, plan->tstride) *
-            plan->tstride;
+    const size_t need = sdp_es::bucket_table_entries(
+            sdp_es::num_chunks(num_vis, plan->tstride), plan->nbins,
+            plan->nsbins);
     if (need > s.table_entries)
     {
         if (s.table) SDP_HIP_CHECK(hipFree(s.table), status);
