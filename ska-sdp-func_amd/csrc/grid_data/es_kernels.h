@@ -28,9 +28,14 @@ constexpr int kCoarseTile = kTile * kCoarse;   // 256 cells
 constexpr int kBinsPerPass = 16384;    // LDS histogram capacity (64 KiB)
 constexpr int kPiece = 4096;           // max entries per scatter work item
 constexpr int kMaxChunks = 1024;       // chunks of visibilities per bucketing
-constexpr int kCountChunks = 4;        // chunks per counting workgroup
+#ifndef SDP_COUNT_CHUNKS
+#define SDP_COUNT_CHUNKS 4
+#endif
+constexpr int kCountChunks = SDP_COUNT_CHUNKS;   // chunks per counting
+                                                 // workgroup
 constexpr int kGroupChunks = 16;       // chunks per level-2 group (and per
                                        // row of the tile count table)
+static_assert(kGroupChunks % kCountChunks == 0, "whole counting workgroups");
 constexpr int kMaxSuperBins = 1024;    // super bins (first bucketing level)
 constexpr int kMaxSuperTiles = 4096;   // tiles per super bin (S^2, S <= 64)
 constexpr int kTapPolyPairs = 3;       // interior taps 1..6 of W = 8

@@ -1257,6 +1257,9 @@ __device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
 // vector operations per operand. Barriers are LDS-only and the next
 // chunk's records load after this chunk's staging (no s_waitcnt vmcnt
 // before the visit loops).
+#ifndef SDP_SCATTER_VSTORE
+#define SDP_SCATTER_VSTORE 1
+#endif
 template<bool DO_W, int NTAP, int CHUNK = 128>
 __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
@@ -1271,8 +1274,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     constexpr int kLead = 16;
     constexpr int kTab = kLead + CHUNK * kStride;
     static_assert(kTab < 65536, "16-bit table indices");
-    __shared__ float s_ku[kTab];
-    __shared__ float2 s_kv[kTab];
+    static_assert(kLead % 4 == 0 && kStride % 4 == 0, "16-byte table rows");
+    __shared__ __attribute__((aligned(16))) float s_ku[kTab];
+    __shared__ __attribute__((aligned(16))) float2 s_kv[kTab];
     __shared__ uint32_t s_list[4][CHUNK + 4];
     // Per entry: byte 0 = row bands hit, byte 1 = column blocks hit (0 for
     // entries past the chunk); s_pos: table index of the entry's row 0 /
@@ -1387,8 +1391,21 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
             {
                 float tu[NTAP];
                 axis_taps<NTAP, true>(p, r.x, u0, u1, tu);
+#if SDP_SCATTER_VSTORE
+                // 16-byte stores (eb is a multiple of 4): entry rows are
+                // kStride = 24 words apart, so a wave's one-word stores of
+                // tap d hit 8 banks (8-way conflicts); quads hit them 2-way.
+                float4* q = reinterpret_cast<float4*>(s_ku + eb);
+#pragma unroll
+                for (int d = 0; d + 4 <= NTAP; d += 4)
+                    q[d / 4] = make_float4(tu[d], tu[d + 1], tu[d + 2],
+                            tu[d + 3]);
+#pragma unroll
+                for (int d = NTAP & ~3; d < NTAP; ++d) s_ku[eb + d] = tu[d];
+#else
 #pragma unroll
                 for (int d = 0; d < NTAP; ++d) s_ku[eb + d] = tu[d];
+#endif
             }
             if (stage_v)
             {
@@ -1396,9 +1413,20 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 axis_taps<NTAP, true>(p, r.y, v0, v1, tv);
                 const bool neg = ((u0 + v0) & 1) != 0;
                 const float zr = neg ? -r.z : r.z, zi = neg ? -r.w : r.w;
+#if SDP_SCATTER_VSTORE
+                float4* q = reinterpret_cast<float4*>(s_kv + eb);
+#pragma unroll
+                for (int d = 0; d + 2 <= NTAP; d += 2)
+                    q[d / 2] = make_float4(tv[d] * zr, tv[d] * zi,
+                            tv[d + 1] * zr, tv[d + 1] * zi);
+                if (NTAP & 1)
+                    s_kv[eb + NTAP - 1] = make_float2(tv[NTAP - 1] * zr,
+                            tv[NTAP - 1] * zi);
+#else
 #pragma unroll
                 for (int d = 0; d < NTAP; ++d)
                     s_kv[eb + d] = make_float2(tv[d] * zr, tv[d] * zi);
+#endif
             }
         }
         // Next chunk's records, issued after this chunk's last use of r so
@@ -1540,31 +1568,12 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
 // evaluated once at staging into LDS tables; visits are packed {entry,
 // u0 - tile row, v0 - tile col} words; the pool is laid out without atomics
 // and the next chunk's records are prefetched.
-#ifndef SDP_GATHER_BALANCE
-#define SDP_GATHER_BALANCE 1
-#endif
-#ifndef SDP_GATHER_XCD
-#define SDP_GATHER_XCD 1
-#endif
-// Work item of workgroup w when the real item count n is known on the
-// device (totals[1]): workgroups are dealt to the 8 XCDs round-robin
-// (w mod 8), so XCD x is given the contiguous item range [x q, (x + 1) q),
-// q = ceil(n / 8): spatially adjacent tiles (consecutive bins) then share
-// an XCD's L2 and the halo rows one tile's gather reads of its neighbours
-// are L2 hits. Workgroups past 8 q find no item.
-__device__ __forceinline__ uint32_t xcd_item(uint32_t w, uint32_t n)
-{
-    const uint32_t q = (n + 7) >> 3;
-    const uint32_t x = w & 7u, k = w >> 3;
-    return k < q ? x * q + k : 0xFFFFFFFFu;
-}
-
 template<bool DO_W, int NTAP>
 __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
         const uint32_t* __restrict__ item_bin, const float* __restrict__ grid,
-        float* __restrict__ vis, const uint32_t* __restrict__ totals)
+        float* __restrict__ vis)
 {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     constexpr int kChunk = 256;
@@ -1578,12 +1587,7 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
     __shared__ float s_acc_im[kChunk];
     __shared__ PoolCounts<kSub * kSub> s_pc;
 
-#if SDP_GATHER_XCD
-    const uint32_t item = xcd_item(blockIdx.x, totals[1]);
-    if (item >= totals[1]) return;
-#else
     const uint32_t item = blockIdx.x;
-#endif
     if (item_bin[item] == kNoBin) return;   // past the last work item
     const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
@@ -1634,8 +1638,7 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         int sub[4], rank[4];
         pool_count<kSub>(s_pc, lane, wave, wlo_r, whi_r, wlo_c, whi_c, sub,
                 rank);
-        lds_barrier();   // B1: previous chunk consumed (LDS only: the
-                         // next records stay in flight)
+        __syncthreads();   // B1: previous chunk consumed
         if (on_plane)
         {
 #pragma clang fp contract(off)
@@ -1653,102 +1656,37 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
         }
         s_acc_re[t] = 0.0f;
         s_acc_im[t] = 0.0f;
-        lds_barrier();   // B2: counts, tables, accumulators ready
+        __syncthreads();   // B2: counts, tables, accumulators ready
         int beg_l, tot_l, base_l;
         pool_layout<kSub * kSub>(s_pc, lane, wave, beg_l, tot_l, base_l);
-        // Visit groups of 16 (one sub-tile each, sub-tile-major). The
-        // chunk's groups are split evenly over the four waves in contiguous
-        // ranges: with sorted records the visits crowd into the few
-        // sub-tiles the chunk's entries start in, so a fixed sub-tile per
-        // wave would leave waves idle at the next barrier. Lane L < 25
-        // holds sub-tile L's group count and inclusive group end.
-        constexpr int kNS = kSub * kSub;
-        const int ng_l = lane < kNS ? (tot_l + 15) >> 4 : 0;
-        int gend_l = ng_l;
-#pragma unroll
-        for (int d = 1; d < 32; d *= 2)
-        {
-            const int y = __shfl_up(gend_l, d, 64);
-            if (lane >= d) gend_l += y;
-        }
-        const int n_groups = __builtin_amdgcn_readlane(gend_l, kNS - 1);
-        const int g0 = (n_groups * wave) >> 2;
-        const int g1 = (n_groups * (wave + 1)) >> 2;
-        // Sub-tile of group g: the number of sub-tiles whose groups end at
-        // or before g (empty sub-tiles end where their predecessor does).
-        auto st_of = [&](int g) -> int {
-            return (int)__popcll(__ballot(lane < kNS && gend_l <= g));
-        };
-#if SDP_GATHER_BALANCE
-        auto st_after = [&](int st) -> int {
-            const int ge = __builtin_amdgcn_readlane(gend_l, st);
-            return ge < g1 ? st_of(ge) : kNS;
-        };
-        const int st_first = g0 < g1 ? st_of(g0) : kNS;
-#else
-        // (A/B: sub-tiles st = wave (mod 4) per wave, whole.)
-        auto next_fixed = [&](int st) -> int {
-            for (; st < kNS; st += 4)
-                if (__builtin_amdgcn_readlane(ng_l, st) != 0) break;
-            return st;
-        };
-        auto st_after = [&](int st) -> int { return next_fixed(st + 4); };
-        const int st_first = next_fixed(wave);
-#endif
-        // A operands straight from the grid (L2 / HBM):
-        // G[r0 + R0 + jl][c0 + C0 + 4 kk + kq], kk = 0..3; the next
-        // sub-tile's are in flight while the current one's visits run.
-        auto load_a = [&](int st, float2 (&v)[4]) {
-            const int R0 = (st / kSub) * 16, C0 = (st % kSub) * 16;
-            const int grow = r0 + R0 + jl;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-            {
-                const int gcol = c0 + C0 + 4 * kk + kq;
-                v[kk] = make_float2(0.0f, 0.0f);
-                if (st < kNS && grow < p.G && gcol < p.G)
-                    v[kk] = g2[(size_t)grow * p.G + gcol];
-            }
-        };
-        int st_cur = st_first;
-        int st_nxt = st_cur < kNS ? st_after(st_cur) : kNS;
-        float2 a_cur[4], a_nxt[4];
-        load_a(st_cur, a_cur);
-        load_a(st_nxt, a_nxt);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
         {
             const int pos = __shfl(base_l, max(sub[k], 0), 64) + rank[k];
             if (sub[k] >= 0) s_pool[pos] = pk;
         }
-        lds_barrier();   // B3: pool complete (the A loads stay in flight)
-        int gg = g0;
-        while (st_cur < kNS)
+        __syncthreads();   // B3: pool complete
+        for (int st = wave; st < kSub * kSub; st += 4)
         {
-            const int sts = __builtin_amdgcn_readfirstlane(st_cur);
+            const int sts = __builtin_amdgcn_readfirstlane(st);
             const int cnt = __builtin_amdgcn_readlane(tot_l, sts);
+            if (cnt == 0) continue;
             const int v_beg = __builtin_amdgcn_readlane(beg_l, sts);
-            const int ge = __builtin_amdgcn_readlane(gend_l, sts);
-            const int gb = ge - __builtin_amdgcn_readlane(ng_l, sts);
             const int R0 = (sts / kSub) * 16, C0 = (sts % kSub) * 16;
+            // A operands straight from the grid (L2 / HBM):
+            // G[r0 + R0 + jl][c0 + C0 + 4 kk + kq], kk = 0..3.
             float a_re[4], a_im[4];
+            const int grow = r0 + R0 + jl;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk)
             {
-                a_re[kk] = a_cur[kk].x;
-                a_im[kk] = a_cur[kk].y;
-                a_cur[kk] = a_nxt[kk];
+                const int gcol = c0 + C0 + 4 * kk + kq;
+                float2 v = make_float2(0.0f, 0.0f);
+                if (grow < p.G && gcol < p.G) v = g2[(size_t)grow * p.G + gcol];
+                a_re[kk] = v.x;
+                a_im[kk] = v.y;
             }
-#if SDP_GATHER_BALANCE
-            const int g_lo = (gg - gb) * 16, g_hi = (min(ge, g1) - gb) * 16;
-#else
-            const int g_lo = 0, g_hi = (ge - gb) * 16;
-#endif
-            gg = ge;
-            st_cur = st_nxt;
-            st_nxt = st_cur < kNS ? st_after(st_cur) : kNS;
-            load_a(st_nxt, a_nxt);
-            for (int g = g_lo; g < g_hi; g += 16)
+            for (int g = 0; g < cnt; g += 16)
             {
 #pragma clang fp contract(off)
                 const bool valid = g + jl < cnt;
@@ -1795,7 +1733,7 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
                 }
             }
         }
-        lds_barrier();
+        __syncthreads();
         if (on_plane)
         {
             const uint64_t idx = (uint64_t)__float_as_uint(r.w);
@@ -2470,9 +2408,6 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         const float* recs = (const float*)s.recs;
         if (p.support <= 16)
         {
-            // XCD-aware mapping (xcd_item): whole rounds of 8 workgroups,
-            // so that every item of the range split is reached.
-            const uint32_t n_gather = (n_items + 7u) & ~7u;
             if (p.support <= 8 && sort_records && sort_pieces())
             {
                 k_sort_pieces<<<n_items, 256, 0, stream>>>(p,
@@ -2481,21 +2416,17 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
                 SDP_HIP_CHECK_LAUNCH(status);
             }
             if (p.support <= 8 && p.do_w)
-                k_gather_tab<true, 9><<<n_gather, 256, 0, stream>>>(p, recs,
-                        s.bin_start, s.item_start, s.item_bin, grid, vis,
-                        s.totals);
+                k_gather_tab<true, 9><<<n_items, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis);
             else if (p.support <= 8)
-                k_gather_tab<false, 9><<<n_gather, 256, 0, stream>>>(p, recs,
-                        s.bin_start, s.item_start, s.item_bin, grid, vis,
-                        s.totals);
+                k_gather_tab<false, 9><<<n_items, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis);
             else if (p.do_w)
-                k_gather_tab<true, 17><<<n_gather, 256, 0, stream>>>(p, recs,
-                        s.bin_start, s.item_start, s.item_bin, grid, vis,
-                        s.totals);
+                k_gather_tab<true, 17><<<n_items, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis);
             else
-                k_gather_tab<false, 17><<<n_gather, 256, 0, stream>>>(p, recs,
-                        s.bin_start, s.item_start, s.item_bin, grid, vis,
-                        s.totals);
+                k_gather_tab<false, 17><<<n_items, 256, 0, stream>>>(p, recs,
+                        s.bin_start, s.item_start, s.item_bin, grid, vis);
             SDP_HIP_CHECK_LAUNCH(status);
             return *status;
         }
