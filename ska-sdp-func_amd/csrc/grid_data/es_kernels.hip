@@ -7,6 +7,7 @@
 // accumulation instead of per-tap HBM atomics).
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 
 #include "utility/wave_ops.h"
 #include "es_kernels.h"
@@ -1745,6 +1746,104 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
     }
 }
 
+// Degrid mode, f32, lane-per-entry form (the default for W <= 8). A work
+// item stages the grid window its entries can reach -- the 64 x 64 tile of
+// their first taps plus the 8 cells a 9-tap support extends past it --
+// into LDS with coalesced row loads, then each thread gathers whole
+// entries: the entry's u and v taps are evaluated once (polynomial
+// interior taps, as the scatter), the 8 (or 9) grid rows of its support
+// are contracted with the v taps and the row sums with the u taps, and the
+// visibility is read-modify-written once. Work per entry: 64 LDS reads and
+// 144 FMAs, with no cross-lane reduction, no sub-tile pools and no record
+// sort; the matrix-core form (k_gather_tab) spends 16 x 16 products per
+// sub-tile visit on 8 x 8 supports.
+template<bool DO_W, int NTAP>
+__global__ __launch_bounds__(256) void k_gather_win(EsParams<float> p,
+        const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
+        const uint32_t* __restrict__ item_start,
+        const uint32_t* __restrict__ item_bin, const float* __restrict__ grid,
+        float* __restrict__ vis)
+{
+    static_assert(NTAP == 9, "window of tile + 8 cells");
+    constexpr int kWin = kTile + NTAP - 1;     // 72 rows / columns
+    constexpr int kPitch = kWin;               // float2 per LDS row
+    __shared__ float2 win[kWin * kPitch];
+    const uint32_t item = blockIdx.x;
+    if (item_bin[item] == kNoBin) return;      // past the last work item
+    const int b = (int)item_bin[item];
+    const uint32_t piece = item - item_start[b];
+    const uint32_t e0 = bin_start[b] + piece * kPiece;
+    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
+    if (e0 >= e1) return;                      // empty tile
+    int r0, c0;
+    tile_origin(p, b, r0, c0);
+    if (r0 >= p.G || c0 >= p.G) return;        // phantom tile
+    const int t = threadIdx.x;
+    const int half = p.G / 2;
+    const int tu0 = r0 - half, tv0 = c0 - half;
+    // This thread's first record, in flight during the window staging.
+    const float4* recs4 = (const float4*)recs;
+    float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (e0 + t < e1) r = recs4[e0 + t];
+    const float2* g2 = (const float2*)grid;
+    for (int k = t; k < kWin * kWin; k += 256)
+    {
+        const int rr = k / kWin, cc = k - rr * kWin;
+        float2 v = make_float2(0.0f, 0.0f);
+        if (r0 + rr < p.G && c0 + cc < p.G)
+            v = g2[(size_t)(r0 + rr) * p.G + c0 + cc];
+        win[rr * kPitch + cc] = v;
+    }
+    __syncthreads();
+    for (uint32_t e = e0 + t; e < e1; e += 256)
+    {
+#pragma clang fp contract(off)
+        const float4 rc = r;
+        if (e + 256 < e1) r = recs4[e + 256];
+        float kw = 1.0f;
+        if (DO_W && !plane_tap(p, fabsf(rc.z), kw)) continue;   // off plane
+        int u0, u1, v0, v1;
+        tap_range(p, rc.x, rc.y, u0, u1, v0, v1);
+        float tu[NTAP], tv[NTAP];
+        axis_taps<NTAP, true>(p, rc.x, u0, u1, tu);
+        axis_taps<NTAP, true>(p, rc.y, v0, v1, tv);
+        const float2* base = win + (u0 - tu0) * kPitch + (v0 - tv0);
+        float sr = 0.0f, si = 0.0f;
+        // The ninth tap of an axis is non-zero only at an exact-integer
+        // position (W + 1 taps); rows / columns of zero taps are skipped.
+        const int nu = u1 - u0 + 1, nv = v1 - v0 + 1;
+#pragma unroll
+        for (int du = 0; du < NTAP; ++du)
+        {
+            if (du >= nu) break;
+            const float2* row = base + du * kPitch;
+            float tr = 0.0f, ti = 0.0f;
+#pragma unroll
+            for (int dv = 0; dv < NTAP - 1; ++dv)
+            {
+                const float2 g = row[dv];
+                tr = __builtin_fmaf(tv[dv], g.x, tr);
+                ti = __builtin_fmaf(tv[dv], g.y, ti);
+            }
+            if (nv == NTAP)
+            {
+                const float2 g = row[NTAP - 1];
+                tr = __builtin_fmaf(tv[NTAP - 1], g.x, tr);
+                ti = __builtin_fmaf(tv[NTAP - 1], g.y, ti);
+            }
+            sr = __builtin_fmaf(tu[du], tr, sr);
+            si = __builtin_fmaf(tu[du], ti, si);
+        }
+        // (-1)^(u0 + v0) of the checkerboard, with the w-tap; the flip
+        // conjugates (kernels.cu:267-268).
+        const float ks = ((u0 + v0) & 1) ? -kw : kw;
+        const uint64_t idx = (uint64_t)__float_as_uint(rc.w);
+        const float flip = signbit(rc.z) ? -1.0f : 1.0f;
+        vis[2 * idx] += sr * ks;
+        vis[2 * idx + 1] += si * ks * flip;
+    }
+}
+
 // Degrid mode, ahead of k_gather_tab: each work item's records reordered
 // by the 16 x 16 sub-tile of their first tap (counting sort over the 16
 // keys, deterministic: key, then round, wave, lane), so that a chunk of
@@ -2384,6 +2483,20 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     return *status;
 }
 
+// f32 gather form for W <= 8: 0 = lane-per-entry window (k_gather_win,
+// default), 1 = matrix-core sub-tile form (k_gather_tab; env
+// SDP_ES_GATHER=mfma).
+int gather_form()
+{
+    static int v = -1;
+    if (v < 0)
+    {
+        const char* e = getenv("SDP_ES_GATHER");
+        v = (e && strcmp(e, "mfma") == 0) ? 1 : 0;
+    }
+    return v;
+}
+
 // Degrid records sorted by first-tap sub-tile inside each work item before
 // k_gather_tab (env SDP_ES_SORT_PIECES=0 disables).
 bool sort_pieces()
@@ -2408,6 +2521,20 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         const float* recs = (const float*)s.recs;
         if (p.support <= 16)
         {
+            if (p.support <= 8 && gather_form() == 0)
+            {
+                // Lane-per-entry window gather (no record sort needed).
+                if (p.do_w)
+                    k_gather_win<true, 9><<<n_items, 256, 0, stream>>>(p,
+                            recs, s.bin_start, s.item_start, s.item_bin,
+                            grid, vis);
+                else
+                    k_gather_win<false, 9><<<n_items, 256, 0, stream>>>(p,
+                            recs, s.bin_start, s.item_start, s.item_bin,
+                            grid, vis);
+                SDP_HIP_CHECK_LAUNCH(status);
+                return *status;
+            }
             if (p.support <= 8 && sort_records && sort_pieces())
             {
                 k_sort_pieces<<<n_items, 256, 0, stream>>>(p,
