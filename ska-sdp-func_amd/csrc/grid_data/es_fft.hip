@@ -1841,16 +1841,18 @@ bool herm_degrid_enabled(const ImageParams<float>& ip)
     return on && !ip.do_w && ip.G >= 2048 && ip.G <= 8192;
 }
 
-// Row pass of the real-output gridding transform in the single-row form
-// (k_rows_herm1 + k_cols_a_herm_pairs) instead of row quads (env
-// SDP_ES_HERM_ROWS=1; A/B).
+// Row passes of the real-output / real-input transforms in the single-row
+// form (k_rows_herm1 + k_cols_a_herm_pairs, k_cols_b_image_herm_pairs +
+// k_rows_image_herm1; the default: A/B at config 2, gridding row + column
+// pass 256 -> 242 us, degridding 236 -> 229 us) instead of row quads (env
+// SDP_ES_HERM_ROWS=0).
 bool herm_rows1()
 {
     static int on = -1;
     if (on < 0)
     {
         const char* e = getenv("SDP_ES_HERM_ROWS");
-        on = (e && e[0] == '1') ? 1 : 0;
+        on = (e && e[0] == '0') ? 0 : 1;
     }
     return on != 0;
 }

@@ -29,7 +29,7 @@ constexpr int kBinsPerPass = 16384;    // LDS histogram capacity (64 KiB)
 constexpr int kPiece = 4096;           // max entries per scatter work item
 constexpr int kMaxChunks = 1024;       // chunks of visibilities per bucketing
 #ifndef SDP_COUNT_CHUNKS
-#define SDP_COUNT_CHUNKS 4
+#define SDP_COUNT_CHUNKS 2
 #endif
 constexpr int kCountChunks = SDP_COUNT_CHUNKS;   // chunks per counting
                                                  // workgroup

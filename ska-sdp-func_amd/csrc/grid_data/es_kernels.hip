@@ -1757,18 +1757,25 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
 // 144 FMAs, with no cross-lane reduction, no sub-tile pools and no record
 // sort; the matrix-core form (k_gather_tab) spends 16 x 16 products per
 // sub-tile visit on 8 x 8 supports.
-template<bool DO_W, int NTAP>
-__global__ __launch_bounds__(256) void k_gather_win(EsParams<float> p,
+// ROWS: the tile rows one workgroup serves (64, or 32: each work item is
+// split over two workgroups by the row of the entries' first tap, so the
+// window is 40 x 72 and twice as many workgroups share a CU); NT threads.
+template<bool DO_W, int NTAP, int ROWS, int NT>
+__global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
         const uint32_t* __restrict__ item_bin, const float* __restrict__ grid,
         float* __restrict__ vis)
 {
     static_assert(NTAP == 9, "window of tile + 8 cells");
-    constexpr int kWin = kTile + NTAP - 1;     // 72 rows / columns
+    static_assert(kTile % ROWS == 0, "whole parts of a tile");
+    constexpr int kParts = kTile / ROWS;
+    constexpr int kWin = kTile + NTAP - 1;     // 72 columns
+    constexpr int kWinR = ROWS + NTAP - 1;     // window rows
     constexpr int kPitch = kWin;               // float2 per LDS row
-    __shared__ float2 win[kWin * kPitch];
-    const uint32_t item = blockIdx.x;
+    __shared__ float2 win[kWinR * kPitch];
+    const uint32_t item = blockIdx.x / kParts;
+    const int part = (int)(blockIdx.x % kParts);
     if (item_bin[item] == kNoBin) return;      // past the last work item
     const int b = (int)item_bin[item];
     const uint32_t piece = item - item_start[b];
@@ -1781,33 +1788,37 @@ __global__ __launch_bounds__(256) void k_gather_win(EsParams<float> p,
     const int t = threadIdx.x;
     const int half = p.G / 2;
     const int tu0 = r0 - half, tv0 = c0 - half;
+    const int rw0 = r0 + part * ROWS;          // first window row (grid)
+    const int ru_lo = part * ROWS;             // entries' first-tap rows
     // This thread's first record, in flight during the window staging.
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (e0 + t < e1) r = recs4[e0 + t];
     const float2* g2 = (const float2*)grid;
-    for (int k = t; k < kWin * kWin; k += 256)
+    for (int k = t; k < kWinR * kWin; k += NT)
     {
         const int rr = k / kWin, cc = k - rr * kWin;
         float2 v = make_float2(0.0f, 0.0f);
-        if (r0 + rr < p.G && c0 + cc < p.G)
-            v = g2[(size_t)(r0 + rr) * p.G + c0 + cc];
+        if (rw0 + rr < p.G && c0 + cc < p.G)
+            v = g2[(size_t)(rw0 + rr) * p.G + c0 + cc];
         win[rr * kPitch + cc] = v;
     }
     __syncthreads();
-    for (uint32_t e = e0 + t; e < e1; e += 256)
+    for (uint32_t e = e0 + t; e < e1; e += NT)
     {
 #pragma clang fp contract(off)
         const float4 rc = r;
-        if (e + 256 < e1) r = recs4[e + 256];
+        if (e + NT < e1) r = recs4[e + NT];
         float kw = 1.0f;
         if (DO_W && !plane_tap(p, fabsf(rc.z), kw)) continue;   // off plane
         int u0, u1, v0, v1;
         tap_range(p, rc.x, rc.y, u0, u1, v0, v1);
+        if (kParts > 1 && (unsigned)(u0 - tu0 - ru_lo) >= (unsigned)ROWS)
+            continue;                          // the other part's entry
         float tu[NTAP], tv[NTAP];
         axis_taps<NTAP, true>(p, rc.x, u0, u1, tu);
         axis_taps<NTAP, true>(p, rc.y, v0, v1, tv);
-        const float2* base = win + (u0 - tu0) * kPitch + (v0 - tv0);
+        const float2* base = win + (u0 - tu0 - ru_lo) * kPitch + (v0 - tv0);
         float sr = 0.0f, si = 0.0f;
         // The ninth tap of an axis is non-zero only at an exact-integer
         // position (W + 1 taps); rows / columns of zero taps are skipped.
@@ -2524,13 +2535,21 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
             if (p.support <= 8 && gather_form() == 0)
             {
                 // Lane-per-entry window gather (no record sort needed).
+#ifndef SDP_WIN_ROWS
+#define SDP_WIN_ROWS 32
+#endif
+#ifndef SDP_WIN_THREADS
+#define SDP_WIN_THREADS 256
+#endif
+                constexpr int kR = SDP_WIN_ROWS, kNT = SDP_WIN_THREADS;
+                const uint32_t nb = n_items * (kTile / kR);
                 if (p.do_w)
-                    k_gather_win<true, 9><<<n_items, 256, 0, stream>>>(p,
-                            recs, s.bin_start, s.item_start, s.item_bin,
+                    k_gather_win<true, 9, kR, kNT><<<nb, kNT, 0, stream>>>(
+                            p, recs, s.bin_start, s.item_start, s.item_bin,
                             grid, vis);
                 else
-                    k_gather_win<false, 9><<<n_items, 256, 0, stream>>>(p,
-                            recs, s.bin_start, s.item_start, s.item_bin,
+                    k_gather_win<false, 9, kR, kNT><<<nb, kNT, 0, stream>>>(
+                            p, recs, s.bin_start, s.item_start, s.item_bin,
                             grid, vis);
                 SDP_HIP_CHECK_LAUNCH(status);
                 return *status;

@@ -937,6 +937,47 @@ struct DftParams
     float2* part;                   // degrid: [visibility][tile] partials
 };
 
+// Tap DFT of a visibility's W kernel taps at one tile row / column:
+// sum_du kt[du] e^{2 pi i (idx + du step) / S} (checkerboard folded into
+// idx and step by the callers). SDP_TOWER_HORNER (default): Horner in
+// z = e^{2 pi i step / S}, then one product with e^{2 pi i idx / S} -- two
+// twiddle-table reads instead of W; the table rows the lanes of a wave read
+// are (a0 + du) l apart, so the W reads per DFT took ~3.5-way LDS bank
+// conflicts on average. f32 rounding of the recurrence: ~W ulp.
+#ifndef SDP_TOWER_HORNER
+#define SDP_TOWER_HORNER 1
+#endif
+__device__ __forceinline__ float2 tap_dft(const float* kt, int W,
+        const float2* s_tw, int idx, int step, int S)
+{
+#pragma clang fp contract(off)
+#if SDP_TOWER_HORNER
+    const float2 z = s_tw[step], e0 = s_tw[idx];
+    float ar = kt[W - 1], ai = 0.0f;
+    for (int du = W - 2; du >= 0; --du)
+    {
+        const float nr = __builtin_fmaf(ar, z.x,
+                __builtin_fmaf(-ai, z.y, kt[du]));
+        const float ni = __builtin_fmaf(ar, z.y, ai * z.x);
+        ar = nr;
+        ai = ni;
+    }
+    return make_float2(__builtin_fmaf(ar, e0.x, -(ai * e0.y)),
+            __builtin_fmaf(ar, e0.y, ai * e0.x));
+#else
+    float sr = 0.0f, si = 0.0f;
+    for (int du = 0; du < W; ++du)
+    {
+        const float2 e = s_tw[idx];
+        sr = __builtin_fmaf(kt[du], e.x, sr);
+        si = __builtin_fmaf(kt[du], e.y, si);
+        idx += step;
+        if (idx >= S) idx -= S;
+    }
+    return make_float2(sr, si);
+#endif
+}
+
 // Ring slots (x .. x + cnt) & (CAP - 1) <- records v0 .. v0 + cnt - 1.
 template<int KWN, int CAP = kDftCap>
 __device__ __forceinline__ void stage_records(const DftParams& d, int64_t v0,
@@ -1118,18 +1159,11 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
                         // for a = a0, a0 + 1, ... the table index advances
                         // by l + S / 2 per tap, the checkerboard included.
                         const uint32_t us = (uint32_t)S;   // a0, l < S
-                        int idx = (int)(((uint32_t)(a0 * l) +
+                        const int idx = (int)(((uint32_t)(a0 * l) +
                                 (uint32_t)((a0 + l) & 1) * (us / 2)) % us);
                         const int step = (int)(((uint32_t)l + us / 2) % us);
-                        float sr = 0.0f, si = 0.0f;
-                        for (int du = 0; du < W; ++du)
-                        {
-                            const float2 e = s_tw[idx];
-                            sr = __builtin_fmaf(kt[du], e.x, sr);
-                            si = __builtin_fmaf(kt[du], e.y, si);
-                            idx += step;
-                            if (idx >= S) idx -= S;
-                        }
+                        const float2 sv = tap_dft(kt, W, s_tw, idx, step, S);
+                        const float sr = sv.x, si = sv.y;
                         if (row)
                         {
                             const float2 vv = s_V[rs];
@@ -1404,19 +1438,11 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                         // Checkerboard folded into the index as in
                         // k_tower_dft.
                         const uint32_t us = (uint32_t)S;   // a0, l < S
-                        int idx = (int)(((uint32_t)(a0 * l) +
+                        const int idx = (int)(((uint32_t)(a0 * l) +
                                 (uint32_t)((a0 + l) & 1) * (us / 2)) % us);
                         const int step = (int)(((uint32_t)l + us / 2) % us);
-                        float sr = 0.0f, si = 0.0f;
-                        for (int du = 0; du < W; ++du)
-                        {
-                            const float2 ew = s_tw[idx];
-                            sr = __builtin_fmaf(kt[du], ew.x, sr);
-                            si = __builtin_fmaf(kt[du], ew.y, si);
-                            idx += step;
-                            if (idx >= S) idx -= S;
-                        }
-                        res = make_float2(sr, -si);   // conjugate
+                        const float2 sv = tap_dft(kt, W, s_tw, idx, step, S);
+                        res = make_float2(sv.x, -sv.y);   // conjugate
                     }
                     if (q < kDftTile) s_ku[rs][q] = res;
                     else s_kv[rs][q - kDftTile] = res;
