@@ -2,9 +2,12 @@
 # Per-kernel VGPR / scratch / occupancy of one HIP source (gfx950).
 # Usage: scripts/kres.sh path/to/file.hip [extra hipcc flags]
 SRC=$1; shift
+case "$SRC" in
+  *es_kernels.hip|*sdp_grid_wstack_wtower.hip) VGPR_FORM="-mllvm -amdgpu-mfma-vgpr-form" ;;
+esac
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics \
-    -I"$ROOT/include" -I"$ROOT/ska-sdp-func_amd/csrc" -x hip -c "$SRC" -o /tmp/kres.o \
+    -I"$ROOT/include" -I"$ROOT/ska-sdp-func_amd/csrc" $VGPR_FORM -x hip -c "$SRC" -o /tmp/kres.o \
     -Rpass-analysis=kernel-resource-usage "$@" 2>&1 | python3 -c '
 import re, sys, subprocess
 cur = None; rows = []

@@ -13,6 +13,10 @@ mkdir -p "$OUT"
 REP=${REPLACES:-$SRC}
 OBJ=build/$(dirname "${REP#csrc/}")/$(basename "$REP").o
 CXXFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -I/root/repo/include -Icsrc -Wall -Wno-unused-result"
+# Per-file flags of the Makefile (MFMA results in VGPRs).
+case "$REP" in
+  *es_kernels.hip|*sdp_grid_wstack_wtower.hip) CXXFLAGS="$CXXFLAGS -mllvm -amdgpu-mfma-vgpr-form" ;;
+esac
 /opt/rocm/bin/hipcc $CXXFLAGS "$@" -x hip -c "$SRC" -o "$OUT/variant.o"
 OBJS=$(find build -name '*.o' | sort | grep -v "^$OBJ\$")
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -L/opt/rocm/lib -lrocfft -Wl,-rpath,/opt/rocm/lib -Wl,-soname,libska_sdp_func.so $OBJS "$OUT/variant.o" -o "$OUT/libska_sdp_func.so"
