@@ -33,8 +33,11 @@ Roofline: the dominant hand-written kernel's algorithmic bytes per launch
 divided by its HIP-event duration (library timing on the launch stream).
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -647,6 +650,30 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
+    # The same algorithmic bytes over rocprofv3's average duration of the
+    # 2-D tile kernel, from the kernel-trace summary committed for this
+    # round (profiles/r*_bench_kernel_stats.csv, same config-2 workload).
+    rocprof = None
+    if dom == "tile_kernel":
+        stats = sorted(glob.glob(os.path.join(ROOT, "profiles",
+                                              "r*_bench_kernel_stats.csv")))
+        if stats:
+            try:
+                with open(stats[-1]) as f:
+                    for r in csv.DictReader(f):
+                        if re.search(rf"k_scatter_tab<false, {W + 1}\b",
+                                     r["Name"]):
+                            avg_ms = float(r["AverageNs"]) * 1e-6
+                            gbs = kern_bytes[dom] / (avg_ms * 1e-3) / 1e9
+                            rocprof = {
+                                "stats_file": os.path.relpath(stats[-1], ROOT),
+                                "avg_launch_ms": round(avg_ms, 4),
+                                "achieved": round(gbs, 1),
+                                "frac": round(gbs / HBM_PEAK_GBS, 4)}
+                            break
+            except (OSError, ValueError, KeyError):
+                rocprof = None
+
     config3 = None
     if not args.no_config3:
         config3 = run_config3(args, torch, dev, dist, world, rank)
@@ -723,6 +750,7 @@ def main():
                                        / HBM_PEAK_GBS, 4)
                                  if traffic and avg.get(dom) else None),
                 "algorithmic_bytes_per_launch": kern_bytes[dom],
+                "rocprof": rocprof,
             },
             "call_roofline": {
                 "algorithmic_bytes": gridding_bytes(args.rows, args.chan, G,

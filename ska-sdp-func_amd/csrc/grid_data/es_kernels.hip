@@ -1261,15 +1261,27 @@ __device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
 #ifndef SDP_SCATTER_VSTORE
 #define SDP_SCATTER_VSTORE 1
 #endif
-template<bool DO_W, int NTAP, int CHUNK = 128>
-__global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
+// Entries per chunk (<= 128: u taps staged by threads 0-127, v taps by
+// 128-255; 256: both axes per thread). The tap tables take 0.29 KB per
+// entry: 128 entries = 40 KB of LDS per workgroup (4 per CU), 96 = 30 KB (5).
+#ifndef SDP_SCATTER_NE
+#define SDP_SCATTER_NE 128
+#endif
+#ifndef SDP_SCATTER_WAVES
+#define SDP_SCATTER_WAVES 1
+#endif
+template<bool DO_W, int NTAP, int CHUNK = SDP_SCATTER_NE>
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
         const uint32_t* __restrict__ item_bin, float* __restrict__ grid,
         int flags)
 {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
-    static_assert(CHUNK == 128 || CHUNK == 256, "one or two threads per entry");
+    static_assert(CHUNK == 256 || (CHUNK <= 128 && CHUNK % 16 == 0),
+            "one or two threads per entry");
+    constexpr int kHalf = CHUNK == 256 ? 256 : 128;   // threads per axis
     constexpr int kVec = DO_W ? 2 : 1;
     constexpr int kStride = NTAP + 15;
     constexpr int kLead = 16;
@@ -1308,9 +1320,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     const int lane = t & 63, wave = t >> 6;
     const int i = lane & 15, kq = lane >> 4;
     const int sub_r = wave * 16;
-    const int et = t & (CHUNK - 1);               // this thread's entry
-    const bool stage_u = CHUNK == 256 || t < CHUNK;
-    const bool stage_v = CHUNK == 256 || t >= CHUNK;
+    const int et = t & (kHalf - 1);               // this thread's entry
+    const bool stage_u = CHUNK == 256 || t < 128;
+    const bool stage_v = CHUNK == 256 || t >= 128;
     f32x4 acc_re[4], acc_im[4];
 #pragma unroll
     for (int cblk = 0; cblk < 4; ++cblk)
@@ -1325,7 +1337,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     }
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rw = r;
-    if (e0 + et < e1)
+    if (et < CHUNK && e0 + et < e1)
     {
         r = recs4[(size_t)(e0 + et) * kVec];
         if (DO_W) rw = recs4[(size_t)(e0 + et) * kVec + 1];
@@ -1378,7 +1390,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
             s_info[et] = rm | cm << 8;
             s_pos[et] = pu16 | pv16 << 16;
         }
-        else
+        else if (et < CHUNK)
         {
             uint8_t* info8 = (uint8_t*)s_info;
             uint16_t* pos16 = (uint16_t*)s_pos;
@@ -1432,7 +1444,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         }
         // Next chunk's records, issued after this chunk's last use of r so
         // that nothing waits for them before the next staging.
-        if (cb + CHUNK + et < e1)
+        if (et < CHUNK && cb + CHUNK + et < e1)
         {
             r = recs4[(size_t)(cb + CHUNK + et) * kVec];
             if (DO_W) rw = recs4[(size_t)(cb + CHUNK + et) * kVec + 1];
@@ -1440,12 +1452,14 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         lds_barrier();   // B2: entry words and tap tables complete
         uint32_t* list = s_list[wave];
         // The chunk's entry words, read once for the four column blocks.
-        uint32_t inf[CHUNK / 64], ps[CHUNK / 64];
+        constexpr int kGroups = (CHUNK + 63) / 64;
+        uint32_t inf[kGroups], ps[kGroups];
 #pragma unroll
-        for (int gi = 0; gi < CHUNK / 64; ++gi)
+        for (int gi = 0; gi < kGroups; ++gi)
         {
-            inf[gi] = s_info[gi * 64 + lane];
-            ps[gi] = s_pos[gi * 64 + lane];
+            const bool in = CHUNK % 64 == 0 || gi * 64 + lane < CHUNK;
+            inf[gi] = in ? s_info[gi * 64 + lane] : 0u;
+            ps[gi] = in ? s_pos[gi * 64 + lane] : 0u;
         }
         const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
@@ -1459,7 +1473,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                     ((uint32_t)(cblk * 16 - 64) << 16);
             int cnt = 0;
 #pragma unroll
-            for (int gi = 0; gi < CHUNK / 64; ++gi)
+            for (int gi = 0; gi < kGroups; ++gi)
             {
                 const bool hit = (inf[gi] >> wave) & (inf[gi] >> (8 + cblk)) & 1u;
                 const uint64_t m = __ballot(hit);

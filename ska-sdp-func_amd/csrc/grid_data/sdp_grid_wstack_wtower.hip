@@ -880,10 +880,11 @@ __device__ __forceinline__ Cx<double> pattern_pow_f32(double turns, int e)
 // per call by k_dft_prep instead of being rebuilt by every tile's
 // workgroup (which cost three dependent global round trips per staging
 // pass: record, uvw, kernel rows): words [0] iu0 (-1: invalid), [1] iv0,
-// [2] P (w-layer, tower numbering), [3] unused, [4, 6) V, then the W u taps
-// and W v taps (f32, zero if invalid), then 16 w taps keyed by absolute
-// w-layer, (P + j) % 16 (zeros elsewhere).
-constexpr int kPrepHdr = 6;
+// [2] P (w-layer, tower numbering), [3] unused, [4, 6) V, [6, 8) zero, then
+// the W u taps and W v taps (f32, zero if invalid; the u taps start on a
+// 16-byte boundary), then 16 w taps keyed by absolute w-layer, (P + j) % 16
+// (zeros elsewhere). Records are copied whole into the LDS ring.
+constexpr int kPrepHdr = 8;
 __host__ __device__ constexpr int prep_stride(int W)
 {
     return (kPrepHdr + 2 * W + 16 + 3) & ~3;
@@ -947,6 +948,7 @@ struct DftParams
 #ifndef SDP_TOWER_HORNER
 #define SDP_TOWER_HORNER 1
 #endif
+
 __device__ __forceinline__ float2 tap_dft(const float* kt, int W,
         const float2* s_tw, int idx, int step, int S)
 {
@@ -978,28 +980,59 @@ __device__ __forceinline__ float2 tap_dft(const float* kt, int W,
 #endif
 }
 
-// Ring slots (x .. x + cnt) & (CAP - 1) <- records v0 .. v0 + cnt - 1.
-template<int KWN, int CAP = kDftCap>
-__device__ __forceinline__ void stage_records(const DftParams& d, int64_t v0,
-        int x, int cnt, int W, int t, int (*s_tap)[2], float2* s_V,
-        float (*s_kuv)[32], float (*s_kw)[KWN])
+// Same, W known at compile time (the common W = 8): the tap reads are
+// 16-byte aligned rows (kPrepHdr = 8) and the loop is unrolled.
+template<int WT>
+__device__ __forceinline__ float2 tap_dft_w(const float* kt,
+        const float2* s_tw, int idx, int step)
 {
-    const int stride = d.prep_stride;
-    const float* src = d.prep + v0 * stride;
-    const int total = cnt * stride;
-    for (int o = t; o < total; o += 256)
+#pragma clang fp contract(off)
+    const float* k = static_cast<const float*>(__builtin_assume_aligned(kt, 16));
+    const float2 z = s_tw[step], e0 = s_tw[idx];
+    float ar = k[WT - 1], ai = 0.0f;
+#pragma unroll
+    for (int du = WT - 2; du >= 0; --du)
     {
-        const int vi = o / stride, w = o - vi * stride;
-        const int rs = (x + vi) & (CAP - 1);
-        const float f = src[o];
-        if (w < 2) s_tap[rs][w] = __float_as_int(f);
-        else if (w < 4) continue;
-        else if (w < kPrepHdr)
-        {
-            if (s_V) reinterpret_cast<float*>(&s_V[rs])[w - 4] = f;
-        }
-        else if (w < kPrepHdr + 2 * W) s_kuv[rs][w - kPrepHdr] = f;
-        else if (w < kPrepHdr + 2 * W + 16) s_kw[rs][w - kPrepHdr - 2 * W] = f;
+        const float nr = __builtin_fmaf(ar, z.x, __builtin_fmaf(-ai, z.y, k[du]));
+        const float ni = __builtin_fmaf(ar, z.y, ai * z.x);
+        ar = nr;
+        ai = ni;
+    }
+    return make_float2(__builtin_fmaf(ar, e0.x, -(ai * e0.y)),
+            __builtin_fmaf(ar, e0.y, ai * e0.x));
+}
+
+__device__ __forceinline__ float2 tap_dft_any(const float* kt, int W,
+        const float2* s_tw, int idx, int step, int S)
+{
+#if SDP_TOWER_HORNER
+    if (W == 8) return tap_dft_w<8>(kt, s_tw, idx, step);
+#endif
+    return tap_dft(kt, W, s_tw, idx, step, S);
+}
+
+// Staged records in LDS: ring slot rs holds visibility record words
+// [0, prep_stride) (layout above) at a pitch of 60 words = 4 x 15, so that
+// the 16 different slots a quarter-wave reads at one word offset fall on
+// 16 different banks.
+constexpr int kRecPitch = 60;
+static_assert(prep_stride(16) <= kRecPitch, "records of W <= 16 fit a slot");
+
+// Ring slots (x .. x + cnt) & (CAP - 1) <- records v0 .. v0 + cnt - 1:
+// 16-byte copies, 16 threads per record (no per-word branches).
+template<int CAP>
+__device__ __forceinline__ void stage_records(const DftParams& d, int64_t v0,
+        int x, int cnt, int t, float (*s_rec)[kRecPitch])
+{
+    const int nq = d.prep_stride / 4;
+    const float4* src = reinterpret_cast<const float4*>(d.prep +
+            v0 * d.prep_stride);
+    for (int o = t; o < cnt * 16; o += 256)
+    {
+        const int vi = o >> 4, k = o & 15;
+        if (k < nq)
+            *reinterpret_cast<float4*>(&s_rec[(x + vi) & (CAP - 1)][4 * k]) =
+                    src[vi * nq + k];
     }
 }
 
@@ -1020,15 +1053,14 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
     __shared__ int s_start[kDftLayers + 1];
     __shared__ float2 s_aku[kDftCap][kDftTile];     // V KU(l), tile rows
     __shared__ float2 s_kv[kDftCap][kCols];         // KV(m), tile columns
-    // w taps keyed by absolute w-layer: s_kw[rs][(P + j) % 16] = kw_j,
-    // so the rank update reads kw at layer L without first reading P.
-    __shared__ float s_kw[kDftCap][16];
-    __shared__ int s_tap[kDftCap][2];   // iu0 (-1: invalid), iv0
-    __shared__ float s_kuv[kDftCap][32];            // u taps, then v taps
-    __shared__ float2 s_V[kDftCap];
+    // Staged records: iu0 (-1: invalid), iv0, V, u taps, v taps, and the
+    // w taps keyed by absolute w-layer, word kwo + (P + j) % 16 = kw_j, so
+    // the rank update reads kw at layer L without first reading P.
+    __shared__ __attribute__((aligned(16))) float s_rec[kDftCap][kRecPitch];
 
     const TowerParams& tp = d.tp;
     const int S = tp.S, ws = tp.w_support, W = tp.support;
+    const int kwo = kPrepHdr + 2 * W;   // w taps in a staged record
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int tiles_v = S / kCols;
     const int L0 = (blockIdx.x / tiles_v) * kDftTile;
@@ -1137,8 +1169,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
                 lds_sync();   // ring slots free
                 // Copy the staged visibilities' records (one dependent
                 // global load per word, 16-byte coalesced) into the ring.
-                stage_records(d, s0 + x, x, cnt, W, t, s_tap, s_V, s_kuv,
-                        s_kw);
+                stage_records<kDftCap>(d, s0 + x, x, cnt, t, s_rec);
                 lds_sync();
                 constexpr int kPer = kDftTile + kCols;   // rows, columns
                 for (int o = t; o < cnt * kPer; o += 256)
@@ -1146,13 +1177,13 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
                     const int v = x + (int)((unsigned)o / kPer);
                     const int rs = v & (kDftCap - 1);
                     const int q = (int)((unsigned)o % kPer);
-                    const int iu0 = s_tap[rs][0];
+                    const int iu0 = __float_as_int(s_rec[rs][0]);
                     float2 res = make_float2(0.0f, 0.0f);
                     if (iu0 >= 0)
                     {
                         const bool row = q < kDftTile;
-                        const int a0 = row ? iu0 : s_tap[rs][1];
-                        const float* kt = s_kuv[rs] + (row ? 0 : W);
+                        const int a0 = row ? iu0 : __float_as_int(s_rec[rs][1]);
+                        const float* kt = &s_rec[rs][kPrepHdr] + (row ? 0 : W);
                         const int l = row ? L0 + q : M0 + q - kDftTile;
                         // (-1)^(a + l) e^{2 pi i a l / S} = e^{2 pi i k / S}
                         // with k = a l + (a + l) S / 2 (mod S; S is even):
@@ -1162,11 +1193,12 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
                         const int idx = (int)(((uint32_t)(a0 * l) +
                                 (uint32_t)((a0 + l) & 1) * (us / 2)) % us);
                         const int step = (int)(((uint32_t)l + us / 2) % us);
-                        const float2 sv = tap_dft(kt, W, s_tw, idx, step, S);
+                        const float2 sv = tap_dft_any(kt, W, s_tw, idx, step, S);
                         const float sr = sv.x, si = sv.y;
                         if (row)
                         {
-                            const float2 vv = s_V[rs];
+                            const float2 vv = *reinterpret_cast<const float2*>(
+                                    &s_rec[rs][4]);
                             res = make_float2(vv.x * sr - vv.y * si,
                                     vv.x * si + vv.y * sr);
                         }
@@ -1187,7 +1219,9 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
                 const bool ok = v < b;
                 const int rs = (ok ? v : a) & (kDftCap - 1);
                 const float2 av = s_aku[rs][bl + i];
-                const float kw = ok ? s_kw[rs][L & 15] : 0.0f;
+                // Unconditional read + select: no exec-mask branch per step.
+                const float kw_rs = s_rec[rs][kwo + (L & 15)];
+                const float kw = ok ? kw_rs : 0.0f;
                 const float ar = av.x * kw, ai = av.y * kw;
 #pragma unroll
                 for (int nb = 0; nb < NB; ++nb)
@@ -1279,13 +1313,12 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
     // quarter-wave, on 16 different rows, then cover all 64 banks once.
     __shared__ float2 s_ku[kCap][kDftTile + 2];  // conj KU(l), tile rows
     __shared__ float2 s_kv[kCap][kCols + 2];     // conj KV(m), tile cols
-    __shared__ float s_kw[kCap][17];             // keyed by w-layer % 16
-    __shared__ int s_tap[kCap][2];
-    __shared__ float s_kuv[kCap][32];
+    __shared__ __attribute__((aligned(16))) float s_rec[kCap][kRecPitch];
     __shared__ float2 s_acc[4][kCap];            // per-wave partials
 
     const TowerParams& tp = d.tp;
     const int S = tp.S, ws = tp.w_support, W = tp.support;
+    const int kwo = kPrepHdr + 2 * W;   // w taps in a staged record
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int tiles_v = S / kCols;
     const int tile = blockIdx.x;
@@ -1418,8 +1451,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                 st_lo = a;
                 st_hi = e;
                 const int cnt = e - x;
-                stage_records<17, kCap>(d, s0 + x, x, cnt, W, t, s_tap, nullptr,
-                        s_kuv, s_kw);
+                stage_records<kCap>(d, s0 + x, x, cnt, t, s_rec);
                 lds_sync();
                 constexpr int kPer = kDftTile + kCols;   // rows, columns
                 for (int o = t; o < cnt * kPer; o += 256)
@@ -1427,13 +1459,13 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                     const int v = x + (int)((unsigned)o / kPer);
                     const int rs = v & (kCap - 1);
                     const int q = (int)((unsigned)o % kPer);
-                    const int iu0 = s_tap[rs][0];
+                    const int iu0 = __float_as_int(s_rec[rs][0]);
                     float2 res = make_float2(0.0f, 0.0f);
                     if (iu0 >= 0)
                     {
                         const bool row = q < kDftTile;
-                        const int a0 = row ? iu0 : s_tap[rs][1];
-                        const float* kt = s_kuv[rs] + (row ? 0 : W);
+                        const int a0 = row ? iu0 : __float_as_int(s_rec[rs][1]);
+                        const float* kt = &s_rec[rs][kPrepHdr] + (row ? 0 : W);
                         const int l = row ? L0 + q : M0 + q - kDftTile;
                         // Checkerboard folded into the index as in
                         // k_tower_dft.
@@ -1441,7 +1473,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                         const int idx = (int)(((uint32_t)(a0 * l) +
                                 (uint32_t)((a0 + l) & 1) * (us / 2)) % us);
                         const int step = (int)(((uint32_t)l + us / 2) % us);
-                        const float2 sv = tap_dft(kt, W, s_tw, idx, step, S);
+                        const float2 sv = tap_dft_any(kt, W, s_tw, idx, step, S);
                         res = make_float2(sv.x, -sv.y);   // conjugate
                     }
                     if (q < kDftTile) s_ku[rs][q] = res;
@@ -1507,7 +1539,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                 pi = sdp_hip::sum_rows16(pi);
                 if (kq == 0 && ok)
                 {
-                    const float kw = s_kw[rs][L & 15];
+                    const float kw = s_rec[rs][kwo + (L & 15)];
                     float2 acc = s_acc[wave][rs];
                     acc.x += pr * kw;
                     acc.y += pi * kw;
@@ -1665,6 +1697,8 @@ __global__ void k_dft_prep(const int4* __restrict__ vrec, int64_t n,
     }
     r[4] = vre;
     r[5] = vim;
+    r[6] = 0.0f;
+    r[7] = 0.0f;
     for (int j = 0; j < W; ++j)
     {
         r[kPrepHdr + j] = tt.valid ? (float)uv_kernel[tt.u_off + j] : 0.0f;
