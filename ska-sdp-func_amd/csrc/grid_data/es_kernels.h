@@ -81,9 +81,10 @@ void es_tap_poly_fit(double beta_f32, float out[kTapPolyPairs]
 // Scratch owned by a plan (device pointers).
 struct BucketScratch
 {
-    uint32_t* table = nullptr;      // [chunks][nsbins] super-bin counts /
-                                    // offsets, then [groups][nbins] tile
-                                    // counts / offsets (bucket_table_entries)
+    uint32_t* table = nullptr;      // [groups][nbins] tile counts / offsets
+                                    // from the start, [chunks][nsbins]
+                                    // super-bin counts / offsets at the end
+                                    // (bucket_table_entries)
     uint32_t* bin_count = nullptr;  // [tstride]: tile then super-bin totals
     uint32_t* bin_start = nullptr;  // [nbins + 1]
     uint32_t* item_start = nullptr; // [nbins + 1]
@@ -95,6 +96,7 @@ struct BucketScratch
     void* recs1 = nullptr;          // first level, by super bin (same size)
     size_t recs_bytes = 0;
     size_t table_entries = 0;
+    bool gtable_dirty = true;       // group rows not known to be zero
 };
 
 // Number of visibility chunks used for a given visibility count and count

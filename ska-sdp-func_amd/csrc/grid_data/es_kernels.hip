@@ -345,14 +345,26 @@ __global__ __launch_bounds__(NT) void k_bucket_count(EsParams<T> p,
 }
 
 // Per bin: exclusive prefix over chunks (in place) and the bin total.
-// Block = 16 waves; lane = bin, wave = contiguous range of chunks.
+// Block = 16 waves; lane = bin, wave = contiguous range of chunks. One
+// launch scans two tables: blocks [0, nblk) the first, the rest the second.
 __global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
-        int num_chunks, int nbins, uint32_t* __restrict__ bin_count)
+        int num_chunks, int nbins, uint32_t* __restrict__ bin_count,
+        int nblk, uint32_t* table2, int num_chunks2, int nbins2,
+        uint32_t* __restrict__ bin_count2)
 {
     // nbins = columns = the table row length (tile and super-bin counts).
     __shared__ uint32_t part[16][64];
+    int bx = blockIdx.x;
+    if (bx >= nblk)
+    {
+        table = table2;
+        num_chunks = num_chunks2;
+        nbins = nbins2;
+        bin_count = bin_count2;
+        bx -= nblk;
+    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int b = blockIdx.x * 64 + lane;
+    const int b = bx * 64 + lane;
     const int per = (num_chunks + 15) / 16;
     const int c0 = __builtin_amdgcn_readfirstlane(wave * per);
     const int c1 = min(num_chunks, c0 + per);
@@ -851,7 +863,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(
 template<typename T, int MODE, bool DO_W>
 __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
         const uint32_t* __restrict__ stable,
-        const uint32_t* __restrict__ gtable,
+        uint32_t* __restrict__ gtable,
         const uint32_t* __restrict__ bin_count,
         const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ sb_start, const T* __restrict__ recs1,
@@ -872,7 +884,11 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
         if (tu < p.ntiles && tv < p.ntiles)
         {
             const int f = fine_bin(p, tu, tv);
-            cur[j] = bin_start[f] + gtable[(size_t)blockIdx.x * p.nbins + f];
+            uint32_t* g = gtable + (size_t)blockIdx.x * p.nbins + f;
+            cur[j] = bin_start[f] + *g;
+            // This block is the entry's only reader: leave the table zeroed
+            // for the next bucketing's atomic counts (no memset per call).
+            *g = 0u;
         }
     }
     __syncthreads();
@@ -2339,17 +2355,17 @@ template<typename T, int MODE, bool DO_W, int NT>
 void launch_fill(int nc, int64_t chunk, const EsParams<T>& p,
         int64_t num_rows, int num_chan, const T* uvw, const T* freq,
         const T* vis, const T* weight, const BucketScratch* s,
-        hipStream_t stream)
+        const uint32_t* stable, uint32_t* gtable, hipStream_t stream)
 {
     k_bucket_fill1<T, MODE, DO_W, NT><<<nc, NT, 0, stream>>>(p, num_rows,
-            num_chan, chunk, uvw, freq, vis, weight, s->table, s->bin_count,
+            num_chan, chunk, uvw, freq, vis, weight, stable, s->bin_count,
             s->sb_start, (T*)s->recs1);
     // Chunk groups x super bins: each block moves the records of one
     // group of kGroupChunks chunks of one super bin.
     const int ng = (nc + kGroupChunks - 1) / kGroupChunks;
     k_bucket_fill2<T, MODE, DO_W><<<dim3(ng, p.nsbins), 256, 0, stream>>>(
-            p, nc, s->table, s->table + (size_t)nc * p.nsbins, s->bin_count,
-            s->bin_start, s->sb_start, (const T*)s->recs1, (T*)s->recs);
+            p, nc, stable, gtable, s->bin_count, s->bin_start, s->sb_start,
+            (const T*)s->recs1, (T*)s->recs);
 }
 
 #define SDP_ES_BY_THREADS(NTV, CALL) \
@@ -2377,8 +2393,14 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
     const int passes = (p.nbins + kBinsPerPass - 1) / kBinsPerPass;
     const dim3 grid_b((nc + kCountChunks - 1) / kCountChunks, passes);
     const int ng = (nc + kGroupChunks - 1) / kGroupChunks;
-    uint32_t* stable = s->table;                       // [nc][nsbins]
-    uint32_t* gtable = s->table + (size_t)nc * p.nsbins;   // [ng][nbins]
+    // Group tile counts from the start of the table, chunk super-bin counts
+    // from its end: for any two calls whose table needs fit the allocation
+    // (need grows with nc, ng with nc) one's chunk rows never overlap the
+    // other's group rows, so the group rows stay zero between calls (each
+    // is cleared by its k_bucket_fill2 reader).
+    uint32_t* gtable = s->table;                                   // [ng][nbins]
+    uint32_t* stable = s->table + s->table_entries -
+            (size_t)nc * p.nsbins;                                 // [nc][nsbins]
     const int nt = bucket_threads();
     if (p.nsbins < 1 || p.nsbins > kMaxSuperBins ||
             (1 << (2 * p.sshift)) > kMaxSuperTiles ||
@@ -2388,9 +2410,13 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
         SDP_LOG_ERROR("Bucketing geometry / count table mismatch");
         return SDP_ERR_RUNTIME;
     }
-    // The group rows of tile counts are accumulated atomically.
-    SDP_HIP_CHECK(hipMemsetAsync(gtable, 0, (size_t)ng * p.nbins *
-            sizeof(uint32_t), stream), status);
+    // The group rows of tile counts are accumulated atomically into a zeroed
+    // table: zeroed here only after an allocation or an interrupted call.
+    if (s->gtable_dirty)
+        SDP_HIP_CHECK(hipMemsetAsync(s->table, 0, s->table_entries *
+                sizeof(uint32_t), stream), status);
+    if (*status) return *status;
+    s->gtable_dirty = true;
     if (mode == MODE_GRID)
         SDP_ES_BY_THREADS(nt, (launch_count<T, MODE_GRID, NT>(grid_b, p,
                 num_rows, num_chan, chunk, nc, uvw, freq, stable, gtable,
@@ -2403,11 +2429,9 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
     // Column prefixes (in place) and totals: tile counts over the chunk
     // groups into bin_count[0, nbins), super-bin counts over the chunks
     // into bin_count[nbins, nbins + nsbins).
-    k_scan_columns<<<(p.nbins + 63) / 64, 1024, 0, stream>>>(
-            gtable, ng, p.nbins, s->bin_count);
-    SDP_HIP_CHECK_LAUNCH(status);
-    k_scan_columns<<<(p.nsbins + 63) / 64, 1024, 0, stream>>>(
-            stable, nc, p.nsbins, s->bin_count + p.nbins);
+    const int gblk = (p.nbins + 63) / 64, sblk = (p.nsbins + 63) / 64;
+    k_scan_columns<<<gblk + sblk, 1024, 0, stream>>>(gtable, ng, p.nbins,
+            s->bin_count, gblk, stable, nc, p.nsbins, s->bin_count + p.nbins);
     SDP_HIP_CHECK_LAUNCH(status);
     k_scan_bins<<<1, 1024, 0, stream>>>(s->bin_count, p.nbins,
             s->bin_start, s->item_start, s->totals, s->item_bin,
@@ -2431,19 +2455,20 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
         if (p.do_w)
             SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_GRID, true, NT>(nc,
                     chunk, p, num_rows, num_chan, uvw, freq, vis, weight, s,
-                    stream)))
+                    stable, gtable, stream)))
         else
             SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_GRID, false, NT>(nc,
                     chunk, p, num_rows, num_chan, uvw, freq, vis, weight, s,
-                    stream)))
+                    stable, gtable, stream)))
     }
     else
     {
         SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_DEGRID, false, NT>(nc,
                 chunk, p, num_rows, num_chan, uvw, freq, vis, weight, s,
-                stream)))
+                stable, gtable, stream)))
     }
     SDP_HIP_CHECK_LAUNCH(status);
+    if (!*status) s->gtable_dirty = false;
     return *status;
 }
 

@@ -276,6 +276,7 @@ void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
         s.table = nullptr;
         SDP_HIP_CHECK(hipMalloc(&s.table, need * sizeof(uint32_t)), status);
         s.table_entries = *status ? 0 : need;
+        s.gtable_dirty = true;
     }
 }
 
