@@ -1790,6 +1790,12 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
 // ROWS: the tile rows one workgroup serves (64, or 32: each work item is
 // split over two workgroups by the row of the entries' first tap, so the
 // window is 40 x 72 and twice as many workgroups share a CU); NT threads.
+#ifndef SDP_WIN_STAGE_V2
+#define SDP_WIN_STAGE_V2 1
+#endif
+#ifndef SDP_WIN_CONTRACT_V2
+#define SDP_WIN_CONTRACT_V2 1
+#endif
 template<bool DO_W, int NTAP, int ROWS, int NT>
 __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
@@ -1824,6 +1830,44 @@ __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (e0 + t < e1) r = recs4[e0 + t];
+#if SDP_WIN_STAGE_V2
+    // The window as 16-byte loads (two cells; c0 and G are even), all of a
+    // thread's loads issued before the first LDS store: one memory latency
+    // per work item instead of one per loop trip. Buffer loads relative to
+    // the window's first row (32-bit offsets for any G); cells past the grid
+    // address beyond the range and load zeros.
+    {
+        constexpr int kQ = kWin / 2;                 // float4 per window row
+        constexpr int kN4 = kWinR * kQ;
+        constexpr int kPer = (kN4 + NT - 1) / NT;
+        const size_t row_f2 = (size_t)p.G;
+        const float* wbase = grid + 2 * (size_t)rw0 * row_f2;
+        const uint32_t nrows = (uint32_t)min(kWinR, p.G - rw0);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<float*>(wbase), 0, (int)(nrows * row_f2 * 8u),
+                0x00020000);
+        float4 wv[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+        {
+            const int k = t + j * NT;
+            const int rr = k / kQ, cq = k - rr * kQ;
+            const bool in = k < kN4 && c0 + 2 * cq < p.G;
+            const uint32_t off = in ? (uint32_t)((rr * row_f2 + c0 + 2 * cq)
+                    * 8u) : 0xFFFFFFF0u;
+            wv[j] = __builtin_bit_cast(float4,
+                    __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        }
+#pragma unroll
+        for (int j = 0; j < kPer; ++j)
+        {
+            const int k = t + j * NT;
+            const int rr = k / kQ, cq = k - rr * kQ;
+            if (k < kN4)
+                *reinterpret_cast<float4*>(&win[rr * kPitch + 2 * cq]) = wv[j];
+        }
+    }
+#else
     const float2* g2 = (const float2*)grid;
     for (int k = t; k < kWinR * kWin; k += NT)
     {
@@ -1833,6 +1877,7 @@ __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
             v = g2[(size_t)(rw0 + rr) * p.G + c0 + cc];
         win[rr * kPitch + cc] = v;
     }
+#endif
     __syncthreads();
     for (uint32_t e = e0 + t; e < e1; e += NT)
     {
@@ -1850,30 +1895,67 @@ __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
         axis_taps<NTAP, true>(p, rc.y, v0, v1, tv);
         const float2* base = win + (u0 - tu0 - ru_lo) * kPitch + (v0 - tv0);
         float sr = 0.0f, si = 0.0f;
-        // The ninth tap of an axis is non-zero only at an exact-integer
-        // position (W + 1 taps); rows / columns of zero taps are skipped.
-        const int nu = u1 - u0 + 1, nv = v1 - v0 + 1;
-#pragma unroll
-        for (int du = 0; du < NTAP; ++du)
+        // 2-D: the unrolled form (92 VGPRs, 5 waves per SIMD) measured
+        // 447 -> 438 us at config 2; 3-D (plane-tap divergence): the row
+        // loop (70 VGPRs, 7 waves) 391 vs 403 us.
+        if constexpr (SDP_WIN_CONTRACT_V2 && !DO_W)
         {
-            if (du >= nu) break;
-            const float2* row = base + du * kPitch;
-            float tr = 0.0f, ti = 0.0f;
+            // The ninth tap of an axis is non-zero only at an exact-integer
+            // position (W + 1 taps, rare): the wave takes the 9 x 9 form
+            // only if one of its entries has one (taps past u1 / v1 are zero
+            // and the window holds the rows / columns they address), else
+            // 8 x 8. Fully unrolled: tap registers with constant indices.
+            const bool nine = u1 - u0 + 1 == NTAP || v1 - v0 + 1 == NTAP;
+            auto contract = [&](auto n_c) {
+                constexpr int N = decltype(n_c)::value;
 #pragma unroll
-            for (int dv = 0; dv < NTAP - 1; ++dv)
+                for (int du = 0; du < N; ++du)
+                {
+                    const float2* row = base + du * kPitch;
+                    float tr = 0.0f, ti = 0.0f;
+#pragma unroll
+                    for (int dv = 0; dv < N; ++dv)
+                    {
+                        const float2 g = row[dv];
+                        tr = __builtin_fmaf(tv[dv], g.x, tr);
+                        ti = __builtin_fmaf(tv[dv], g.y, ti);
+                    }
+                    sr = __builtin_fmaf(tu[du], tr, sr);
+                    si = __builtin_fmaf(tu[du], ti, si);
+                }
+            };
+            if (__ballot(nine))
+                contract(std::integral_constant<int, NTAP>{});
+            else
+                contract(std::integral_constant<int, NTAP - 1>{});
+        }
+        else
+        {
+            // The ninth tap of an axis is non-zero only at an exact-integer
+            // position (W + 1 taps); rows / columns of zero taps are skipped.
+            const int nu = u1 - u0 + 1, nv = v1 - v0 + 1;
+#pragma unroll
+            for (int du = 0; du < NTAP; ++du)
             {
-                const float2 g = row[dv];
-                tr = __builtin_fmaf(tv[dv], g.x, tr);
-                ti = __builtin_fmaf(tv[dv], g.y, ti);
+                if (du >= nu) break;
+                const float2* row = base + du * kPitch;
+                float tr = 0.0f, ti = 0.0f;
+#pragma unroll
+                for (int dv = 0; dv < NTAP - 1; ++dv)
+                {
+                    const float2 g = row[dv];
+                    tr = __builtin_fmaf(tv[dv], g.x, tr);
+                    ti = __builtin_fmaf(tv[dv], g.y, ti);
+                }
+                if (nv == NTAP)
+                {
+                    const float2 g = row[NTAP - 1];
+                    tr = __builtin_fmaf(tv[NTAP - 1], g.x, tr);
+                    ti = __builtin_fmaf(tv[NTAP - 1], g.y, ti);
+                }
+                sr = __builtin_fmaf(tu[du], tr, sr);
+                si = __builtin_fmaf(tu[du], ti, si);
             }
-            if (nv == NTAP)
-            {
-                const float2 g = row[NTAP - 1];
-                tr = __builtin_fmaf(tv[NTAP - 1], g.x, tr);
-                ti = __builtin_fmaf(tv[NTAP - 1], g.y, ti);
-            }
-            sr = __builtin_fmaf(tu[du], tr, sr);
-            si = __builtin_fmaf(tu[du], ti, si);
         }
         // (-1)^(u0 + v0) of the checkerboard, with the w-tap; the flip
         // conjugates (kernels.cu:267-268).
