@@ -878,6 +878,27 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
     const int S = 1 << p.sshift;
     const int su = sb / p.nsuper, sv = sb - su * p.nsuper;
     const int tu_base = su << p.sshift, tv_base = sv << p.sshift;
+    const uint32_t* col = stable + sb;
+    const uint32_t sbs = sb_start[sb];
+    const uint32_t e0 = sbs + col[(size_t)c0 * p.nsbins];
+    const uint32_t e1 = c1 < nc ? sbs + col[(size_t)c1 * p.nsbins] :
+            sb_start[sb + 1];
+    // Four records per thread in flight (loads issued before the LDS
+    // atomics and stores of the first). Gridding: the first round's loads
+    // are issued before the tile cursors are set up, so that the two
+    // overlap (108 -> 102 us 2-D, 210 -> 191 us 3-D at config 2; the degrid
+    // records measured 84 -> 90 us that way).
+    constexpr bool kEarly = MODE == MODE_GRID;
+    constexpr int kIn = 4;
+    T rec[kIn][kWords];
+    auto load = [&](uint32_t e) {
+#pragma unroll
+        for (int q = 0; q < kIn; ++q)
+            if (e + q * 256 < e1)
+                copy_rec<T, kWords>(rec[q],
+                        recs1 + (size_t)(e + q * 256) * kWords);
+    };
+    if (kEarly) load(e0 + t);
     for (int j = t; j < S * S; j += 256)
     {
         const int tu = tu_base + (j >> p.sshift), tv = tv_base + (j & (S - 1));
@@ -892,20 +913,9 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
         }
     }
     __syncthreads();
-    const uint32_t* col = stable + sb;
-    const uint32_t e0 = sb_start[sb] + col[(size_t)c0 * p.nsbins];
-    const uint32_t e1 = c1 < nc ? sb_start[sb] + col[(size_t)c1 * p.nsbins] :
-            sb_start[sb + 1];
-    // Four records per thread in flight (loads issued before the LDS
-    // atomics and stores of the first).
-    constexpr int kIn = 4;
     for (uint32_t e = e0 + t; e < e1; e += 256 * kIn)
     {
-        T rec[kIn][kWords];
-#pragma unroll
-        for (int q = 0; q < kIn; ++q)
-            if (e + q * 256 < e1)
-                copy_rec<T, kWords>(rec[q], recs1 + (size_t)(e + q * 256) * kWords);
+        if (!kEarly || e != e0 + t) load(e);
 #pragma unroll
         for (int q = 0; q < kIn; ++q)
         {
