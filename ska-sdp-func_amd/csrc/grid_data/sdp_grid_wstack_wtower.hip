@@ -900,6 +900,21 @@ __host__ __device__ constexpr int prep_stride(int W)
 #ifndef TOWER_IDFT_WAVES
 #define TOWER_IDFT_WAVES 6
 #endif
+// k_tower_dft with 8 waves of one block each (SDP_DFT_NW=8): half the
+// per-lane pixel state, so more waves per SIMD hide the per-layer
+// dependency chains.
+#ifndef TOWER_DFT8_WAVES
+#define TOWER_DFT8_WAVES 6
+#endif
+#ifndef TOWER_IDFT8_WAVES
+#define TOWER_IDFT8_WAVES 8
+#endif
+#ifndef SDP_IDFT_NW
+#define SDP_IDFT_NW 4
+#endif
+#ifndef SDP_DFT_NW
+#define SDP_DFT_NW 4
+#endif
 // k_tower_idft: staged visibilities (ring) and w-layers between re-anchored
 // images (see k_tower_idft).
 #ifndef SDP_IDFT_CAP
@@ -1020,14 +1035,14 @@ static_assert(prep_stride(16) <= kRecPitch, "records of W <= 16 fit a slot");
 
 // Ring slots (x .. x + cnt) & (CAP - 1) <- records v0 .. v0 + cnt - 1:
 // 16-byte copies, 16 threads per record (no per-word branches).
-template<int CAP>
+template<int CAP, int NT = 256>
 __device__ __forceinline__ void stage_records(const DftParams& d, int64_t v0,
         int x, int cnt, int t, float (*s_rec)[kRecPitch])
 {
     const int nq = d.prep_stride / 4;
     const float4* src = reinterpret_cast<const float4*>(d.prep +
             v0 * d.prep_stride);
-    for (int o = t; o < cnt * 16; o += 256)
+    for (int o = t; o < cnt * 16; o += NT)
     {
         const int vi = o >> 4, k = o & 15;
         if (k < nq)
@@ -1040,14 +1055,18 @@ __device__ __forceinline__ void stage_records(const DftParams& d, int64_t v0,
 // 32 x (32 NB) pixel tile; with NB = 2 each wave's two blocks share the row
 // taps (A operand) and the per-layer window / Horner bookkeeping, and their
 // independent accumulation chains keep the matrix core busier.
-template<typename U, int NB>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower_dft(
+template<typename U, int NB, int NW = 4>
+__global__ __launch_bounds__(64 * NW)
+__attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_DFT8_WAVES :
+        NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower_dft(
         DftParams d,
         const U* __restrict__ uvws, const Cx<float>* __restrict__ vis)
 {
 #pragma clang fp contract(off)
-    constexpr int kCols = kDftTile * NB;             // tile columns
+    // NW waves: NW / 2 per 16-row block band, NB 16 x 16 blocks each.
+    constexpr int NT = 64 * NW, kCW = NW / 2;
+    constexpr int kNbOff = 16 * kCW;                 // column step of nb
+    constexpr int kCols = kNbOff * NB;               // tile columns
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     extern __shared__ float2 s_tw[];                // e^{2 pi i k / S}, S
     __shared__ int s_start[kDftLayers + 1];
@@ -1069,11 +1088,11 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
     const int64_t gs = d.gslot_base + slot;
     const int s0 = d.seg_start[gs], s1 = d.seg_end[gs];
     const int n = s1 - s0;
-    // This lane's pixels: block (wave >> 1, wave & 1) of the tile, MFMA
+    // This lane's pixels: block (wave / kCW, wave % kCW) of the tile, MFMA
     // C layout: rows 4 (lane >> 4) + r, column lane & 15.
-    const int bl = (wave >> 1) * 16, bm = (wave & 1) * 16;
+    const int bl = (wave / kCW) * 16, bm = (wave % kCW) * 16;
     const int i = lane & 15, kq = lane >> 4;
-    const int pm = M0 + bm + i;       // column of block 0; block nb: + 32 nb
+    const int pm = M0 + bm + i;       // column of block 0; block nb: + kNbOff nb
     // The recurrence wimg = wimg / D + M_L runs in f32 within blocks of
     // kDftBlock layers (acc32, 1 / D rounded to f32) and in f64 across
     // blocks (acc64 = acc64 / D^kDftBlock + acc32): the reference keeps
@@ -1094,7 +1113,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
         for (int r = 0; r < 4; ++r)
         {
             const int64_t e = (int64_t)(L0 + bl + 4 * kq + r) * S + pm +
-                    kDftTile * nb;
+                    kNbOff * nb;
             acc[nb][r] = cx<double>(0.0, 0.0);
             const Cx<double> di = d.wp_inv[e];
             dinv32[nb][r] = make_float2((float)di.re, (float)di.im);
@@ -1108,11 +1127,11 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
         for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                out[(int64_t)(L0 + bl + 4 * kq + r) * S + pm + kDftTile * nb] =
+                out[(int64_t)(L0 + bl + 4 * kq + r) * S + pm + kNbOff * nb] =
                         cx<float>(0, 0);
         return;
     }
-    for (int k = t; k < S; k += 256) s_tw[k] = d.tw[k];
+    for (int k = t; k < S; k += NT) s_tw[k] = d.tw[k];
     // Layer starts: s_start[k] = first visibility with P >= P_first + k.
     // w-layers in the tower's numbering (TowerParams::w_plane).
     const int shift = (int)(d.P0 - tp.off_w);
@@ -1123,7 +1142,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
         s_start[0] = 0;
         s_start[npl] = n;
     }
-    for (int v = t + 1; v < n; v += 256)
+    for (int v = t + 1; v < n; v += NT)
     {
         const int pa = d.vrec[s0 + v - 1].z + shift - P_first;
         const int pb = d.vrec[s0 + v].z + shift - P_first;
@@ -1169,10 +1188,10 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
                 lds_sync();   // ring slots free
                 // Copy the staged visibilities' records (one dependent
                 // global load per word, 16-byte coalesced) into the ring.
-                stage_records<kDftCap>(d, s0 + x, x, cnt, t, s_rec);
+                stage_records<kDftCap, NT>(d, s0 + x, x, cnt, t, s_rec);
                 lds_sync();
                 constexpr int kPer = kDftTile + kCols;   // rows, columns
-                for (int o = t; o < cnt * kPer; o += 256)
+                for (int o = t; o < cnt * kPer; o += NT)
                 {
                     const int v = x + (int)((unsigned)o / kPer);
                     const int rs = v & (kDftCap - 1);
@@ -1226,7 +1245,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
 #pragma unroll
                 for (int nb = 0; nb < NB; ++nb)
                 {
-                    const float2 bv = s_kv[rs][bm + kDftTile * nb + i];
+                    const float2 bv = s_kv[rs][bm + kNbOff * nb + i];
                     a_re[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.x,
                             a_re[nb], 0, 0, 0);
                     a_re[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(-ai, bv.y,
@@ -1264,7 +1283,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
 #pragma unroll
         for (int r = 0; r < 4; ++r)
         {
-            const int pl = L0 + bl + 4 * kq + r, pc = pm + kDftTile * nb;
+            const int pl = L0 + bl + 4 * kq + r, pc = pm + kNbOff * nb;
             const int64_t e = (int64_t)pl * S + pc;
             Cx<double> z = acc[nb][r];
             if (e_final != 0) z = cmul(z, pattern_pow_f32(d.w_turns[e], e_final));
@@ -1296,13 +1315,17 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower
 // NB: 16 x 16 pixel blocks per wave along the columns (tile 32 x 32 NB);
 // with NB = 2 a wave's two blocks extend the contraction T = Y conj(KV) over
 // 32 columns before the one row contraction / partial update per chunk.
-template<typename U, int NB>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_tower_idft(
+template<typename U, int NB, int NW = 4>
+__global__ __launch_bounds__(64 * NW)
+__attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_IDFT8_WAVES :
+        NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_tower_idft(
         DftParams d, const U* __restrict__ uvws)
 {
 #pragma clang fp contract(off)
-    constexpr int kCols = kDftTile * NB;             // tile columns
+    // NW waves: NW / 2 per 16-row block band, NB 16 x 16 blocks each.
+    constexpr int NT = 64 * NW, kCW = NW / 2;
+    constexpr int kNbOff = 16 * kCW;                 // column step of nb
+    constexpr int kCols = kNbOff * NB;               // tile columns
     constexpr int kCap = SDP_IDFT_CAP, kBlk = SDP_IDFT_BLOCK;
     static_assert((kCap & (kCap - 1)) == 0 && kCap >= 16, "ring of >= 16");
     using f32x4 = __attribute__((ext_vector_type(4))) float;
@@ -1314,7 +1337,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
     __shared__ float2 s_ku[kCap][kDftTile + 2];  // conj KU(l), tile rows
     __shared__ float2 s_kv[kCap][kCols + 2];     // conj KV(m), tile cols
     __shared__ __attribute__((aligned(16))) float s_rec[kCap][kRecPitch];
-    __shared__ float2 s_acc[4][kCap];            // per-wave partials
+    __shared__ float2 s_acc[NW][kCap];           // per-wave partials
 
     const TowerParams& tp = d.tp;
     const int S = tp.S, ws = tp.w_support, W = tp.support;
@@ -1330,7 +1353,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
     const int n = s1 - s0;
     if (n <= 0) return;
     const int ntiles = (S / kDftTile) * tiles_v;
-    const int bl = (wave >> 1) * 16, bm = (wave & 1) * 16;
+    const int bl = (wave / kCW) * 16, bm = (wave % kCW) * 16;
     const int i = lane & 15, kq = lane >> 4;
     const int shift = (int)(d.P0 - tp.off_w);
     const int P_first = d.vrec[s0].z + shift, P_last = d.vrec[s1 - 1].z + shift;
@@ -1355,7 +1378,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
             for (int kk = 0; kk < 4; ++kk)
             {
                 const int pr = L0 + bl + i;
-                const int pc = M0 + kDftTile * nb + bm + 4 * kq + kk;
+                const int pc = M0 + kNbOff * nb + bm + 4 * kq + kk;
                 const int64_t e = (int64_t)pr * S + pc;
                 // Input checkerboard and 1 / S^2 of the sub-grid inverse
                 // FFT (.cpp:423-427), in single precision as the reference's
@@ -1380,20 +1403,20 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
         for (int kk = 0; kk < 4; ++kk)
         {
             const int pr = L0 + bl + i;
-            const int pc = M0 + kDftTile * nb + bm + 4 * kq + kk;
+            const int pc = M0 + kNbOff * nb + bm + 4 * kq + kk;
             const Cx<double> di = d.wp_inv[(int64_t)pr * S + pc];
             dinv32[nb][kk] = make_float2((float)di.re, (float)di.im);
         }
     anchor(L_first);
-    for (int k = t; k < S; k += 256) s_tw[k] = d.tw[k];
-    for (int k = t; k < 4 * kCap; k += 256)
+    for (int k = t; k < S; k += NT) s_tw[k] = d.tw[k];
+    for (int k = t; k < NW * kCap; k += NT)
         s_acc[k / kCap][k & (kCap - 1)] = make_float2(0.0f, 0.0f);
     if (t == 0)
     {
         s_start[0] = 0;
         s_start[npl] = n;
     }
-    for (int v = t + 1; v < n; v += 256)
+    for (int v = t + 1; v < n; v += NT)
     {
         const int pa = d.vrec[s0 + v - 1].z + shift - P_first;
         const int pb = d.vrec[s0 + v].z + shift - P_first;
@@ -1404,19 +1427,19 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
 
     // Adds the partials of staged visibilities [f0, f1) to their scratch
     // rows and clears them (call between barriers). Visibility v is always
-    // flushed by thread v % 256, so a scratch entry's read-modify-writes
+    // flushed by thread v % NT, so a scratch entry's read-modify-writes
     // stay in one thread's program order. A visibility is flushed again
     // only when a window wider than the ring re-stages it; below fl_hi
     // (the end of everything flushed so far) the entry is added to, above
     // it stored (the scratch rows start zeroed either way).
     int fl_hi = 0;
     auto flush = [&](int f0, int f1) {
-        for (int v = f0 + ((t - f0) % 256 + 256) % 256; v < f1; v += 256)
+        for (int v = f0 + ((t - f0) % NT + NT) % NT; v < f1; v += NT)
         {
             const int rs = v & (kCap - 1);
             float2 sum = make_float2(0.0f, 0.0f);
 #pragma unroll
-            for (int w = 0; w < 4; ++w)
+            for (int w = 0; w < NW; ++w)
             {
                 sum.x += s_acc[w][rs].x;
                 sum.y += s_acc[w][rs].y;
@@ -1451,10 +1474,10 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                 st_lo = a;
                 st_hi = e;
                 const int cnt = e - x;
-                stage_records<kCap>(d, s0 + x, x, cnt, t, s_rec);
+                stage_records<kCap, NT>(d, s0 + x, x, cnt, t, s_rec);
                 lds_sync();
                 constexpr int kPer = kDftTile + kCols;   // rows, columns
-                for (int o = t; o < cnt * kPer; o += 256)
+                for (int o = t; o < cnt * kPer; o += NT)
                 {
                     const int v = x + (int)((unsigned)o / kPer);
                     const int rs = v & (kCap - 1);
@@ -1504,7 +1527,7 @@ __attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_towe
                     float2 bv[4];
 #pragma unroll
                     for (int kk = 0; kk < 4; ++kk)
-                        bv[kk] = s_kv[rs][kDftTile * nb + bm + 4 * kq + kk];
+                        bv[kk] = s_kv[rs][kNbOff * nb + bm + 4 * kq + kk];
 #pragma unroll
                     for (int kk = 0; kk < 4; ++kk)
                     {
@@ -2405,7 +2428,11 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                 const int tiles = (g.S / kDftTile) *
                         (g.S / (two ? 2 * kDftTile : kDftTile));
                 tower_timing().start();
-                if (two)
+                if (two && SDP_DFT_NW == 8)
+                    k_tower_dft<U, 1, 8><<<dim3(tiles, (unsigned)gr.slots),
+                            512, g.S * sizeof(float2)>>>(dp, d_uvw,
+                            (const Cx<float>*)d_vis);
+                else if (two)
                     k_tower_dft<U, 2><<<dim3(tiles, (unsigned)gr.slots),
                             256, g.S * sizeof(float2)>>>(dp, d_uvw,
                             (const Cx<float>*)d_vis);
@@ -2704,7 +2731,10 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
                 dp.in = (const Cx<float>*)d_wimg;
                 dp.part = d_part;
                 tower_timing().start();
-                if (two)
+                if (two && SDP_IDFT_NW == 8)
+                    k_tower_idft<U, 1, 8><<<dim3(ntiles, (unsigned)gr.slots),
+                            512, g.S * sizeof(float2)>>>(dp, d_uvw);
+                else if (two)
                     k_tower_idft<U, 2><<<dim3(ntiles, (unsigned)gr.slots),
                             256, g.S * sizeof(float2)>>>(dp, d_uvw);
                 else
