@@ -947,12 +947,18 @@ k_rows_herm1(float2* __restrict__ grid, int k0, int M,
 #ifndef SDP_PAIRS_WAVES
 #define SDP_PAIRS_WAVES 2
 #endif
-template<int N1, int N2>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_PAIRS_WAVES)))
+// Threads per workgroup of the paired column pass A: 256 = 32 columns of
+// 8 threads (256-byte row segments), 512 = 64 columns (512 bytes).
+#ifndef SDP_PAIRS_THREADS
+#define SDP_PAIRS_THREADS 256
+#endif
+template<int N1, int N2, int NTH = SDP_PAIRS_THREADS>
+__global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(SDP_PAIRS_WAVES)))
 k_cols_a_herm_pairs(float2* __restrict__ grid, int M,
         const float2* __restrict__ W)
 {
-    constexpr int G = 2 * N1 * N2, B = ColPlan<N2>::B, PT = ColPlan<N2>::P;
+    constexpr int PT = ColPlan<N2>::P, B = NTH / PT;
+    constexpr int G = 2 * N1 * N2;
     using F = ColFft<N2, 1>;
     static_assert(F::EPT == 16 && PT * 16 == N2, "element n2 = p + PT r");
     extern __shared__ float2 lds[];
@@ -1746,14 +1752,15 @@ int col_rounds()
 }
 
 template<auto Kernel>
-dim3 col_grid(int fixed, int M, int B)
+dim3 col_grid(int fixed, int M, int B, int threads = 256,
+        size_t lds = kColLdsBytes)
 {
     static int occ = 0;
     if (!occ)
     {
         int n = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, Kernel, 256,
-                kColLdsBytes) != hipSuccess || n <= 0)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, Kernel, threads,
+                lds) != hipSuccess || n <= 0)
             n = 3;
         occ = n;
     }
@@ -1892,9 +1899,14 @@ int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
                     grid, g.k0, g.M, W, tiles ? occ : nullptr);
             SDP_HIP_CHECK_LAUNCH(&st);
             if (st) return st;
+            constexpr int kTh = SDP_PAIRS_THREADS;
+            constexpr size_t kLds = kColLdsBytes * (kTh / 256);
+            SDP_HIP_CHECK((allow_lds<k_cols_a_herm_pairs<HS::N1, HS::N2>>(
+                    kLds)), &st);
+            if (st) return st;
             const dim3 cg = col_grid<k_cols_a_herm_pairs<HS::N1, HS::N2>>(
-                    HS::N1 / 2 + 1, g.M, ColPlan<HS::N2>::B);
-            k_cols_a_herm_pairs<HS::N1, HS::N2><<<cg, 256, kColLdsBytes,
+                    HS::N1 / 2 + 1, g.M, kTh / ColPlan<HS::N2>::P, kTh, kLds);
+            k_cols_a_herm_pairs<HS::N1, HS::N2><<<cg, kTh, kLds,
                     stream>>>(grid, g.M, W);
             SDP_HIP_CHECK_LAUNCH(&st);
             return st;
