@@ -915,10 +915,6 @@ __host__ __device__ constexpr int prep_stride(int W)
 #ifndef SDP_DFT_NW
 #define SDP_DFT_NW 4
 #endif
-// k_tower_dft with the layer sum lagging one layer behind the matrix ops.
-#ifndef SDP_DFT_LAG
-#define SDP_DFT_LAG 0
-#endif
 // k_tower_idft: staged visibilities (ring) and w-layers between re-anchored
 // images (see k_tower_idft).
 #ifndef SDP_IDFT_CAP
@@ -1105,10 +1101,7 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_DFT8_WAVES :
     // The f32 block partial lives in the matrix-core accumulators: each
     // layer first scales it by 1 / D, then the layer's rank update is
     // accumulated onto it (no zeroing / read-back of a separate layer sum).
-    Cx<double> acc[NB][4];
-#if !SDP_DFT_LAG
-    Cx<double> dinv_k[NB][4];
-#endif
+    Cx<double> acc[NB][4], dinv_k[NB][4];
     float2 dinv32[NB][4];
     f32x4 a_re[NB], a_im[NB];
 #pragma unroll
@@ -1124,9 +1117,7 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_DFT8_WAVES :
             acc[nb][r] = cx<double>(0.0, 0.0);
             const Cx<double> di = d.wp_inv[e];
             dinv32[nb][r] = make_float2((float)di.re, (float)di.im);
-#if !SDP_DFT_LAG
             dinv_k[nb][r] = cpow_int(di, kDftBlock);
-#endif
         }
     }
     Cx<float>* out = d.out + (int64_t)slot * S * S;
@@ -1164,168 +1155,6 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_DFT8_WAVES :
     // Blocks end at L_last: the first block takes the remainder.
     const int n_layers = L_last - L_first + 1;
     const int blk_off = (kDftBlock - n_layers % kDftBlock) % kDftBlock;
-    // Rank-n update of the staged window [lo, hi) of layer L into (ur, ui).
-    auto rank_update = [&](int L, int lo, int hi, f32x4 (&ur)[NB],
-            f32x4 (&ui)[NB]) {
-            for (int a = lo; a < hi; a += kDftCap)
-            {
-                const int b = min(hi, a + kDftCap);
-                if (!(a >= st_lo && b <= st_hi))
-                {
-                    // Stage ahead: fill the ring with [a, a + kDftCap), keeping
-                    // what is already there (windows only move forward, so a
-                    // staging pass serves the next few w-layers; each pass
-                    // costs several dependent global round trips).
-                    const int e = min(n, a + kDftCap);
-                    const int x = (a >= st_lo && a <= st_hi) ? st_hi : a;
-                    st_lo = a;
-                    st_hi = e;
-                    const int cnt = e - x;
-                    lds_sync();   // ring slots free
-                    // Copy the staged visibilities' records (one dependent
-                    // global load per word, 16-byte coalesced) into the ring.
-                    stage_records<kDftCap, NT>(d, s0 + x, x, cnt, t, s_rec);
-                    lds_sync();
-                    constexpr int kPer = kDftTile + kCols;   // rows, columns
-                    for (int o = t; o < cnt * kPer; o += NT)
-                    {
-                        const int v = x + (int)((unsigned)o / kPer);
-                        const int rs = v & (kDftCap - 1);
-                        const int q = (int)((unsigned)o % kPer);
-                        const int iu0 = __float_as_int(s_rec[rs][0]);
-                        float2 res = make_float2(0.0f, 0.0f);
-                        if (iu0 >= 0)
-                        {
-                            const bool row = q < kDftTile;
-                            const int a0 = row ? iu0 : __float_as_int(s_rec[rs][1]);
-                            const float* kt = &s_rec[rs][kPrepHdr] + (row ? 0 : W);
-                            const int l = row ? L0 + q : M0 + q - kDftTile;
-                            // (-1)^(a + l) e^{2 pi i a l / S} = e^{2 pi i k / S}
-                            // with k = a l + (a + l) S / 2 (mod S; S is even):
-                            // for a = a0, a0 + 1, ... the table index advances
-                            // by l + S / 2 per tap, the checkerboard included.
-                            const uint32_t us = (uint32_t)S;   // a0, l < S
-                            const int idx = (int)(((uint32_t)(a0 * l) +
-                                    (uint32_t)((a0 + l) & 1) * (us / 2)) % us);
-                            const int step = (int)(((uint32_t)l + us / 2) % us);
-                            const float2 sv = tap_dft_any(kt, W, s_tw, idx, step, S);
-                            const float sr = sv.x, si = sv.y;
-                            if (row)
-                            {
-                                const float2 vv = *reinterpret_cast<const float2*>(
-                                        &s_rec[rs][4]);
-                                res = make_float2(vv.x * sr - vv.y * si,
-                                        vv.x * si + vv.y * sr);
-                            }
-                            else
-                            {
-                                res = make_float2(sr, si);
-                            }
-                        }
-                        if (q < kDftTile) s_aku[rs][q] = res;
-                        else s_kv[rs][q - kDftTile] = res;
-                    }
-                    lds_sync();
-                }
-                // Complex rank-(b - a) update, four visibilities per step.
-                for (int c4 = a; c4 < b; c4 += 4)
-                {
-                    const int v = c4 + kq;
-                    const bool ok = v < b;
-                    const int rs = (ok ? v : a) & (kDftCap - 1);
-                    const float2 av = s_aku[rs][bl + i];
-                    // Unconditional read + select: no exec-mask branch per step.
-                    const float kw_rs = s_rec[rs][kwo + (L & 15)];
-                    const float kw = ok ? kw_rs : 0.0f;
-                    const float ar = av.x * kw, ai = av.y * kw;
-    #pragma unroll
-                    for (int nb = 0; nb < NB; ++nb)
-                    {
-                        const float2 bv = s_kv[rs][bm + kNbOff * nb + i];
-                        ur[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.x,
-                                ur[nb], 0, 0, 0);
-                        ur[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(-ai, bv.y,
-                                ur[nb], 0, 0, 0);
-                        ui[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.y,
-                                ui[nb], 0, 0, 0);
-                        ui[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ai, bv.x,
-                                ui[nb], 0, 0, 0);
-                    }
-                }
-            }
-    };
-#if SDP_DFT_LAG
-    // Layer L's rank update goes into a fresh accumulator pair while the
-    // f32 block sum takes in layer L - 1's (a = a / D + T[L-1]): the 1 / D
-    // step no longer waits for the matrix ops just issued (the two pairs
-    // alternate between even and odd layers). At a block end the layer's
-    // own pair is added at once, and D^-kDftBlock comes from the f32 1 / D
-    // in double (its rounding, ~kDftBlock ulp of f32 per block, instead of
-    // holding the f64 power in registers).
-    f32x4 t0_re[NB], t0_im[NB], t1_re[NB], t1_im[NB];
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-    {
-        t1_re[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        t1_im[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    }
-    auto layer = [&](int L, f32x4 (&c_re)[NB], f32x4 (&c_im)[NB],
-            f32x4 (&p_re)[NB], f32x4 (&p_im)[NB]) {
-        const int lo = s_start[max(0, min(npl, L - ws + 1 - P_first))];
-        const int hi = s_start[max(0, min(npl, L + 1 - P_first))];
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-        {
-            c_re[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            c_im[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-        rank_update(L, lo, hi, c_re, c_im);
-        auto fold = [&](f32x4 (&x_re)[NB], f32x4 (&x_im)[NB]) {
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    const float xr = a_re[nb][r], xi = a_im[nb][r];
-                    const float2 q = dinv32[nb][r];
-                    a_re[nb][r] = __builtin_fmaf(xr, q.x,
-                            __builtin_fmaf(-xi, q.y, x_re[nb][r]));
-                    a_im[nb][r] = __builtin_fmaf(xr, q.y,
-                            __builtin_fmaf(xi, q.x, x_im[nb][r]));
-                }
-        };
-        fold(p_re, p_im);
-        if ((L - L_first + 1 + blk_off) % kDftBlock == 0)
-        {
-            fold(c_re, c_im);
-#pragma unroll
-            for (int nb = 0; nb < NB; ++nb)
-            {
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                {
-                    Cx<double> q = cx<double>((double)dinv32[nb][r].x,
-                            (double)dinv32[nb][r].y);
-#pragma unroll
-                    for (int k = 1; k < kDftBlock; k *= 2) q = cmul(q, q);
-                    Cx<double> z = cmul(acc[nb][r], q);
-                    z.re += (double)a_re[nb][r];
-                    z.im += (double)a_im[nb][r];
-                    acc[nb][r] = z;
-                }
-                a_re[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-                a_im[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-                c_re[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-                c_im[nb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            }
-        }
-    };
-    for (int L = L_first; L <= L_last; L += 2)
-    {
-        layer(L, t0_re, t0_im, t1_re, t1_im);
-        if (L + 1 <= L_last) layer(L + 1, t1_re, t1_im, t0_re, t0_im);
-    }
-#else
     for (int L = L_first; L <= L_last; ++L)
     {
         const int lo = s_start[max(0, min(npl, L - ws + 1 - P_first))];
@@ -1342,7 +1171,92 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_DFT8_WAVES :
                 a_re[nb][r] = __builtin_fmaf(xr, q.x, -(xi * q.y));
                 a_im[nb][r] = __builtin_fmaf(xr, q.y, xi * q.x);
             }
-        rank_update(L, lo, hi, a_re, a_im);
+        for (int a = lo; a < hi; a += kDftCap)
+        {
+            const int b = min(hi, a + kDftCap);
+            if (!(a >= st_lo && b <= st_hi))
+            {
+                // Stage ahead: fill the ring with [a, a + kDftCap), keeping
+                // what is already there (windows only move forward, so a
+                // staging pass serves the next few w-layers; each pass
+                // costs several dependent global round trips).
+                const int e = min(n, a + kDftCap);
+                const int x = (a >= st_lo && a <= st_hi) ? st_hi : a;
+                st_lo = a;
+                st_hi = e;
+                const int cnt = e - x;
+                lds_sync();   // ring slots free
+                // Copy the staged visibilities' records (one dependent
+                // global load per word, 16-byte coalesced) into the ring.
+                stage_records<kDftCap, NT>(d, s0 + x, x, cnt, t, s_rec);
+                lds_sync();
+                constexpr int kPer = kDftTile + kCols;   // rows, columns
+                for (int o = t; o < cnt * kPer; o += NT)
+                {
+                    const int v = x + (int)((unsigned)o / kPer);
+                    const int rs = v & (kDftCap - 1);
+                    const int q = (int)((unsigned)o % kPer);
+                    const int iu0 = __float_as_int(s_rec[rs][0]);
+                    float2 res = make_float2(0.0f, 0.0f);
+                    if (iu0 >= 0)
+                    {
+                        const bool row = q < kDftTile;
+                        const int a0 = row ? iu0 : __float_as_int(s_rec[rs][1]);
+                        const float* kt = &s_rec[rs][kPrepHdr] + (row ? 0 : W);
+                        const int l = row ? L0 + q : M0 + q - kDftTile;
+                        // (-1)^(a + l) e^{2 pi i a l / S} = e^{2 pi i k / S}
+                        // with k = a l + (a + l) S / 2 (mod S; S is even):
+                        // for a = a0, a0 + 1, ... the table index advances
+                        // by l + S / 2 per tap, the checkerboard included.
+                        const uint32_t us = (uint32_t)S;   // a0, l < S
+                        const int idx = (int)(((uint32_t)(a0 * l) +
+                                (uint32_t)((a0 + l) & 1) * (us / 2)) % us);
+                        const int step = (int)(((uint32_t)l + us / 2) % us);
+                        const float2 sv = tap_dft_any(kt, W, s_tw, idx, step, S);
+                        const float sr = sv.x, si = sv.y;
+                        if (row)
+                        {
+                            const float2 vv = *reinterpret_cast<const float2*>(
+                                    &s_rec[rs][4]);
+                            res = make_float2(vv.x * sr - vv.y * si,
+                                    vv.x * si + vv.y * sr);
+                        }
+                        else
+                        {
+                            res = make_float2(sr, si);
+                        }
+                    }
+                    if (q < kDftTile) s_aku[rs][q] = res;
+                    else s_kv[rs][q - kDftTile] = res;
+                }
+                lds_sync();
+            }
+            // Complex rank-(b - a) update, four visibilities per step.
+            for (int c4 = a; c4 < b; c4 += 4)
+            {
+                const int v = c4 + kq;
+                const bool ok = v < b;
+                const int rs = (ok ? v : a) & (kDftCap - 1);
+                const float2 av = s_aku[rs][bl + i];
+                // Unconditional read + select: no exec-mask branch per step.
+                const float kw_rs = s_rec[rs][kwo + (L & 15)];
+                const float kw = ok ? kw_rs : 0.0f;
+                const float ar = av.x * kw, ai = av.y * kw;
+#pragma unroll
+                for (int nb = 0; nb < NB; ++nb)
+                {
+                    const float2 bv = s_kv[rs][bm + kNbOff * nb + i];
+                    a_re[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.x,
+                            a_re[nb], 0, 0, 0);
+                    a_re[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(-ai, bv.y,
+                            a_re[nb], 0, 0, 0);
+                    a_im[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ar, bv.y,
+                            a_im[nb], 0, 0, 0);
+                    a_im[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(ai, bv.x,
+                            a_im[nb], 0, 0, 0);
+                }
+            }
+        }
         if ((L - L_first + 1 + blk_off) % kDftBlock == 0)
         {
 #pragma unroll
@@ -1361,7 +1275,6 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_DFT8_WAVES :
             }
         }
     }
-#endif
     // End of tower: wimg * D^(L_last - w_support / 2) (.cpp:1102-1113),
     // with the checkerboard of the forward FFT that follows.
     const int e_final = L_last - ws / 2;
