@@ -1287,10 +1287,6 @@ __device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
 #ifndef SDP_SCATTER_VSTORE
 #define SDP_SCATTER_VSTORE 1
 #endif
-// s_setprio 1 around the matrix-op visit loops (A/B switch).
-#ifndef SDP_MFMA_PRIO
-#define SDP_MFMA_PRIO 0
-#endif
 // Entries per chunk (<= 128: u taps staged by threads 0-127, v taps by
 // 128-255; 256: both axes per thread). The tap tables take 0.29 KB per
 // entry: 128 entries = 40 KB of LDS per workgroup (4 per CU), 96 = 30 KB (5).
@@ -1519,9 +1515,6 @@ __attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsPar
             const int n4 = __builtin_amdgcn_readfirstlane(cnt4);
             const int n16 = n4 & ~15;
             f32x4 re = acc_re[cblk], im = acc_im[cblk];
-#if SDP_MFMA_PRIO
-            __builtin_amdgcn_s_setprio(1);
-#endif
             for (int g = n16; g < n4; g += 4)
             {
                 const uint32_t w = list[g + kq];
@@ -1552,9 +1545,6 @@ __attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsPar
                     im = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], bb[s2].y,
                             im, 0, 0, 0);
             }
-#if SDP_MFMA_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
             acc_re[cblk] = re;
             acc_im[cblk] = im;
             // The list is rebuilt for the next column block.

@@ -915,10 +915,6 @@ __host__ __device__ constexpr int prep_stride(int W)
 #ifndef SDP_DFT_NW
 #define SDP_DFT_NW 4
 #endif
-// s_setprio 1 around the matrix-op loops (A/B switch).
-#ifndef SDP_MFMA_PRIO
-#define SDP_MFMA_PRIO 0
-#endif
 // k_tower_idft: staged visibilities (ring) and w-layers between re-anchored
 // images (see k_tower_idft).
 #ifndef SDP_IDFT_CAP
@@ -1236,9 +1232,6 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_DFT8_WAVES :
                 lds_sync();
             }
             // Complex rank-(b - a) update, four visibilities per step.
-#if SDP_MFMA_PRIO
-            __builtin_amdgcn_s_setprio(1);
-#endif
             for (int c4 = a; c4 < b; c4 += 4)
             {
                 const int v = c4 + kq;
@@ -1263,9 +1256,6 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_DFT8_WAVES :
                             a_im[nb], 0, 0, 0);
                 }
             }
-#if SDP_MFMA_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
         }
         if ((L - L_first + 1 + blk_off) % kDftBlock == 0)
         {
@@ -1515,9 +1505,6 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_IDFT8_WAVES :
                 lds_sync();
             }
             // 16 visibilities per step: T = Y_L conj(KV) on the matrix core.
-#if SDP_MFMA_PRIO
-            __builtin_amdgcn_s_setprio(1);
-#endif
             for (int c16 = a; c16 < b; c16 += 16)
             {
                 const int v = c16 + i;
@@ -1582,9 +1569,6 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_IDFT8_WAVES :
                     s_acc[wave][rs] = acc;
                 }
             }
-#if SDP_MFMA_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
         }
         // Y_{L+1} = Y_L / D.
         if ((L + 1 - L_first) % kBlk == 0)
