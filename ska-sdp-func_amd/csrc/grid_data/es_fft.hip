@@ -1751,9 +1751,25 @@ int col_rounds()
     return v;
 }
 
+// The two paired column passes of the real-output form (k_cols_a_herm_pairs,
+// k_cols_b_image_herm_pairs: 2 resident per CU) run 4 rounds (env
+// SDP_ES_PAIR_ROUNDS): config 2, 110.7 -> 105.0 us and 97.6 -> 90.6 us
+// (rounds 1 / 3 / 8: 121.9 / 106.2 / 106.0 and 116.9 / 95.4 / 99.6 us;
+// the other column passes measured flat or slower past 2).
+int pair_rounds()
+{
+    static int v = 0;
+    if (!v)
+    {
+        const char* e = getenv("SDP_ES_PAIR_ROUNDS");
+        v = e ? std::max(1, atoi(e)) : 4;
+    }
+    return v;
+}
+
 template<auto Kernel>
 dim3 col_grid(int fixed, int M, int B, int threads = 256,
-        size_t lds = kColLdsBytes)
+        size_t lds = kColLdsBytes, int rounds = 0)
 {
     static int occ = 0;
     if (!occ)
@@ -1765,7 +1781,7 @@ dim3 col_grid(int fixed, int M, int B, int threads = 256,
         occ = n;
     }
     const int ncb = (M + B - 1) / B;
-    const int want = num_cus() * occ * col_rounds();
+    const int want = num_cus() * occ * (rounds > 0 ? rounds : col_rounds());
     const int split = std::max(1, std::min(ncb, (want + fixed - 1) / fixed));
     return dim3(fixed, split);
 }
@@ -1905,7 +1921,8 @@ int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
                     kLds)), &st);
             if (st) return st;
             const dim3 cg = col_grid<k_cols_a_herm_pairs<HS::N1, HS::N2>>(
-                    HS::N1 / 2 + 1, g.M, kTh / ColPlan<HS::N2>::P, kTh, kLds);
+                    HS::N1 / 2 + 1, g.M, kTh / ColPlan<HS::N2>::P, kTh, kLds,
+                    pair_rounds());
             k_cols_a_herm_pairs<HS::N1, HS::N2><<<cg, kTh, kLds,
                     stream>>>(grid, g.M, W);
             SDP_HIP_CHECK_LAUNCH(&st);
@@ -1996,7 +2013,8 @@ int image_to_grid_herm(const Geometry& g, const float2* W, float2* grid,
         {
             // X formed in column pass B; one row per workgroup iteration.
             const dim3 cg = col_grid<k_cols_b_image_herm_pairs<HS::N1,
-                    HS::N2>>(HS::N2 / 2 + 1, g.M, ColPlan<HS::N1>::B);
+                    HS::N2>>(HS::N2 / 2 + 1, g.M, ColPlan<HS::N1>::B, 256,
+                    kColLdsBytes, pair_rounds());
             k_cols_b_image_herm_pairs<HS::N1, HS::N2><<<cg, 256,
                     kColLdsBytes, stream>>>(grid, g.M, W);
             SDP_HIP_CHECK_LAUNCH(&st);
