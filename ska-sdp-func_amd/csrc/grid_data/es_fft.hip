@@ -1755,7 +1755,8 @@ int col_rounds()
 // k_cols_b_image_herm_pairs: 2 resident per CU) run 4 rounds (env
 // SDP_ES_PAIR_ROUNDS): config 2, 110.7 -> 105.0 us and 97.6 -> 90.6 us
 // (rounds 1 / 3 / 8: 121.9 / 106.2 / 106.0 and 116.9 / 95.4 / 99.6 us;
-// the other column passes measured flat or slower past 2).
+// the other column passes measured flat or slower past 2, except the 3-D
+// column pass B, which takes the same setting).
 int pair_rounds()
 {
     static int v = 0;
@@ -1825,8 +1826,11 @@ int grid_to_image(const Geometry& g, const ImageParams<float>& ip, int plane,
         const float2* W, const float2* grid, float* dirty, hipStream_t stream)
 {
     sdp_Error st = SDP_SUCCESS;
+    // 3-D (w-stacking) planes: four rounds (config-2 geometry, 10 planes:
+    // 167.2 -> 160.5 us per plane; the 2-D form stays on col_rounds()).
     const dim3 blocks = ip.do_w ?
-            col_grid<k_cols_b_grid<N1, N2, true>>(N2, g.M, ColPlan<N1>::B) :
+            col_grid<k_cols_b_grid<N1, N2, true>>(N2, g.M, ColPlan<N1>::B,
+                    256, kColLdsBytes, pair_rounds()) :
             col_grid<k_cols_b_grid<N1, N2, false>>(N2, g.M, ColPlan<N1>::B);
     if (ip.do_w)
         k_cols_b_grid<N1, N2, true><<<blocks, 256, kColLdsBytes, stream>>>(
