@@ -49,6 +49,7 @@ sys.path.insert(0, ROOT)
 
 C_LIGHT = 299792458.0
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3        # MI355X_MICROARCH.md: FP32 vector = f32 MFMA
 
 
 def parse():
@@ -106,6 +107,26 @@ def scatter_bytes(rows, chan, G):
     """Algorithmic HBM bytes of the gridding scatter:
     vis + weight read, uvw read, grid written once."""
     return rows * chan * (8 + 4) + rows * 3 * 4 + chan * 4 + G * G * 8
+
+
+def es_flops_per_vis(W):
+    """SURVEY 8(d) guard roofline: per visibility 2W ES evaluations (exp +
+    sqrt, 2 flops each) + 5 W^2 for the separable tap products and the
+    complex accumulation: 352 at W = 8 (the survey rounds to ~360), 96 at
+    W = 4."""
+    return 5 * W * W + 4 * W
+
+
+def fp32_roofline(n_vis, W, ms):
+    """FP32-vector guard: algorithmic flops of n_vis visibilities over ms
+    against the 157.3 TFLOP/s FP32 peak (vector = f32 matrix rate)."""
+    flops = n_vis * es_flops_per_vis(W)
+    tfs = flops / (ms * 1e-3) / 1e12 if ms else None
+    return {"bound": "fp32", "flops_per_vis": es_flops_per_vis(W),
+            "flops_per_launch": flops,
+            "achieved": round(tfs, 3) if tfs else None,
+            "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tfs / FP32_PEAK_TFLOPS, 4) if tfs else None}
 
 
 def fft_bytes(G):
@@ -234,7 +255,9 @@ def run_config3(args, torch, dev, dist, world, rank):
     the whole call runs on it (no collective). Each reduce is also timed
     alone (reduce_ms)."""
     from ska_sdp_func.grid_data import GridderUvwEsFft
-    from ska_sdp_func.grid_data.distributed import grid_sharded, shard_rows
+    from ska_sdp_func.grid_data.distributed import (grid_sharded,
+                                                    predicted_speedup,
+                                                    shard_rows)
 
     r0, r1 = shard_rows(args.c3_rows, rank, world)
     uvw, freq, vis, weight, px = make_inputs(
@@ -308,6 +331,46 @@ def run_config3(args, torch, dev, dist, world, rank):
                 "reduce_ms": reduce_ms(grid_buf if mode == "grid"
                                        else dirty),
             }
+    # Per-phase device times of one whole call on this rank's shard (HIP
+    # events on the plan stream, summed over the call's row batches),
+    # outside the timed loops: the roofline of the dominant kernel and the
+    # inputs of the scaling model.
+    plan.enable_timing(True)
+    dirty.zero_()
+    plan.grid_uvw_es_fft(uvw, freq, vis, weight, dirty)
+    tm = plan.get_timing() or {}
+    plan.enable_timing(False)
+    sync()
+    phases = {k: round(tm.get(k, 0.0), 4)
+              for k in ("bucket", "tile_kernel", "fft", "image")}
+    n_shard = (r1 - r0) * args.c3_chan
+    t_tile = phases["tile_kernel"]
+    sbytes = scatter_bytes(r1 - r0, args.c3_chan, G)
+    hbm = (sbytes / (t_tile * 1e-3) / 1e9) if t_tile else None
+    roofline = {
+        "kernel": "k_scatter_tab (all row batches of the call)",
+        "bound": "hbm",
+        "achieved": round(hbm, 1) if hbm else None,
+        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(hbm / HBM_PEAK_GBS, 4) if hbm else None,
+        "algorithmic_bytes_per_call": sbytes,
+        "launch_ms": t_tile,
+        "fp32": fp32_roofline(n_shard, plan.support, t_tile),
+        "call_fp32_frac": fp32_roofline(n_shard, plan.support,
+                                        sum(phases.values()))["frac"],
+    }
+    # Strong-scaling model from the one-GPU phases (at N > 1 with the
+    # measured reduce times): the bucketing + tile kernels divide over the
+    # ranks, the FFT + image steps do not.
+    pred = None
+    if world == 1:
+        t_sc = phases["bucket"] + phases["tile_kernel"]
+        t_fi = phases["fft"] + phases["image"]
+        pred = {"n_gpus": 8,
+                "modes": predicted_speedup(t_sc, t_fi, 8, G * G * 8,
+                                           args.image ** 2 * 4),
+                "inputs": {"scatter_ms": round(t_sc, 3),
+                           "fft_image_ms": round(t_fi, 3)}}
     best = max(modes, key=lambda k: modes[k]["mvis_s"])
     out = {
         "workload": (f"ES-FFT gridding, {args.c3_rows} rows x "
@@ -319,6 +382,9 @@ def run_config3(args, torch, dev, dist, world, rank):
         "ms_per_step": modes[best]["ms_per_step"],
         "best_mode": best,
         "modes": modes,
+        "phases_ms": phases,
+        "roofline": roofline,
+        "predicted_8gpu": pred,
         "steps": args.c3_steps,
         "scaling": "strong",
     }
@@ -751,6 +817,13 @@ def main():
                                  if traffic and avg.get(dom) else None),
                 "algorithmic_bytes_per_launch": kern_bytes[dom],
                 "rocprof": rocprof,
+                # SURVEY 8(d) guard: the same launch against the FP32
+                # vector / f32-matrix peak (algorithmic flops per vis).
+                "fp32_frac": (fp32_roofline(total_vis // world, W,
+                                            avg["tile_kernel"])["frac"]
+                              if avg.get("tile_kernel") else None),
+                "fp32": fp32_roofline(total_vis // world, W,
+                                      avg.get("tile_kernel")),
             },
             "call_roofline": {
                 "algorithmic_bytes": gridding_bytes(args.rows, args.chan, G,

@@ -102,7 +102,9 @@ void sdp_gridder_uvw_es_fft_set_max_batch(sdp_GridderUvwEsFft* plan,
         int64_t max_vis);
 int64_t sdp_gridder_uvw_es_fft_batch_vis(const sdp_GridderUvwEsFft* plan);
 
-/* Run the plan's work on a caller-owned hipStream_t (NULL = null stream). */
+/* Run the plan's work on a caller-owned hipStream_t (NULL = null stream).
+ * Switching to another stream first waits for the work queued on the old
+ * one (the plan's grid and scratch are shared by consecutive calls). */
 void sdp_gridder_uvw_es_fft_set_stream(sdp_GridderUvwEsFft* plan,
         void* hip_stream);
 

@@ -13,6 +13,8 @@
 // (exec_shift always runs in place). Host arrays are staged through HBM:
 // the transform itself always runs on the GPU (there is no CPU FFT here).
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 
@@ -451,13 +453,31 @@ void sdp_fft_2d_inplace_permuted(sdp_Mem* data, int is_forward,
                 "GPU array, side a power of two in [1024, 16384]");
         return;
     }
+    // Twiddle tables are built once per grid size and kept for the life of
+    // the process (at most five sizes, 1024..16384; a per-plane caller pays
+    // no allocation). The transform runs on the null stream, as the other
+    // sdp_fft_* kernels here, and returns when it is complete.
+    static std::mutex tw_lock;
+    static std::map<int, sdp_es::FftTwiddles> tw_cache;
+    int e = 0;
     sdp_es::FftTwiddles tw;
-    int e = sdp_es::fft_twiddles_create((int)G, &tw);
+    {
+        std::lock_guard<std::mutex> guard(tw_lock);
+        auto it = tw_cache.find((int)G);
+        if (it == tw_cache.end())
+        {
+            e = sdp_es::fft_twiddles_create((int)G, &tw);
+            if (!e) tw_cache.emplace((int)G, tw);
+        }
+        else
+        {
+            tw = it->second;
+        }
+    }
     if (!e)
         e = sdp_es::fft2d_inplace_permuted((float*)sdp_mem_data(data),
                 (int)G, is_forward != 0, tw, 0);
     if (!e) e = (int)hipStreamSynchronize(0) ? SDP_ERR_RUNTIME : 0;
-    sdp_es::fft_twiddles_destroy(&tw);
     if (e) *status = (sdp_Error)e;
 }
 

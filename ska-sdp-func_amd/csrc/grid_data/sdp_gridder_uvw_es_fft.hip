@@ -407,6 +407,13 @@ void grid_to_image(sdp_GridderUvwEsFft* plan,
 
 // Gridding of rows [0, rows) in batches of rb rows into grid (zeroed
 // first): every batch's tiles are added (the FFT then reads the whole grid).
+// A batched 3-D call re-buckets every batch for every w-plane (planes x
+// batches bucketings instead of batches): a batch's records would have to
+// outlive the plane loop, and the plane's grid must hold every batch before
+// its FFT, so keeping them would need one record array per batch (the
+// scratch the batch limit bounds) or one grid per plane. Bucketing is ~25 %
+// of a 2-D call and less of a 3-D plane; only calls past the batch limit
+// (> 2^28 visibilities by default) pay it.
 template<typename T>
 void scatter_batches(sdp_GridderUvwEsFft* plan, int plane, int64_t rows,
         int64_t rb, int chan, const T* uvw, const T* freq, const T* vis,
@@ -915,7 +922,14 @@ int sdp_gridder_uvw_es_fft_fused_fft(const sdp_GridderUvwEsFft* plan)
 void sdp_gridder_uvw_es_fft_set_stream(sdp_GridderUvwEsFft* plan,
         void* hip_stream)
 {
-    if (plan) plan->stream = (hipStream_t)hip_stream;
+    if (!plan || plan->stream == (hipStream_t)hip_stream) return;
+    // Every call reuses the plan's grid, records and count tables, and the
+    // next bucketing counts into group rows that the previous call's
+    // k_bucket_fill2 clears: the work queued on the old stream must finish
+    // before anything is queued on the new one.
+    if (hipStreamSynchronize(plan->stream) != hipSuccess)
+        plan->scratch.gtable_dirty = true;
+    plan->stream = (hipStream_t)hip_stream;
 }
 
 void sdp_gridder_uvw_es_fft_enable_timing(sdp_GridderUvwEsFft* plan,

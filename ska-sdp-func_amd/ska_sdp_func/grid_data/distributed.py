@@ -70,3 +70,43 @@ def grid_sharded(gridder, uvw, freq, vis, weight, dirty, dist, mode="image",
             gridder.grid_finish(grid_buf, dirty)
         return dirty
     raise ValueError(f"unknown mode {mode!r}")
+
+
+# Bus bandwidth assumed for one RCCL reduce over the xGMI links of an
+# 8-GPU MI355X node when no measurement of the reduce is available (ring
+# reduce: every rank moves (N - 1) / N of the buffer; 7 links of ~153 GB/s
+# per GPU, of which a ring reduce sustains roughly two).
+RING_BUS_GBS = 300.0
+
+
+def reduce_ms_model(nbytes, world, bus_gbs=RING_BUS_GBS):
+    """Modelled time (ms) of one ring reduce of nbytes over world ranks."""
+    if world <= 1:
+        return 0.0
+    return (world - 1) / world * nbytes / (bus_gbs * 1e9) * 1e3
+
+
+def predicted_speedup(t_scatter_ms, t_fft_image_ms, world, grid_bytes,
+                      image_bytes, reduce_ms=None, bus_gbs=RING_BUS_GBS):
+    """Strong-scaling model of one sharded gridding call.
+
+    t_scatter_ms: bucketing + tile kernels of the whole call on one GPU (the
+    part that divides over the ranks); t_fft_image_ms: FFT + image-plane
+    kernels (once per call in mode "grid", once per rank -- concurrently --
+    in mode "image"). reduce_ms: {"grid": ms, "image": ms} measured at this
+    world size, else the ring model above. Returns {mode: speed-up over one
+    GPU, ...} and the modelled per-call times.
+    """
+    t1 = t_scatter_ms + t_fft_image_ms
+    red = dict(reduce_ms or {})
+    out = {}
+    for mode, nbytes in (("grid", grid_bytes), ("image", image_bytes)):
+        r = red.get(mode)
+        if r is None:
+            r = reduce_ms_model(nbytes, world, bus_gbs)
+        t_n = t_scatter_ms / world + r + t_fft_image_ms
+        out[mode] = {"speedup": round(t1 / t_n, 3), "ms": round(t_n, 3),
+                     "reduce_ms": round(r, 3),
+                     "reduce": "measured" if mode in red else
+                               f"model ({bus_gbs:.0f} GB/s ring)"}
+    return out

@@ -189,3 +189,24 @@ def test_shard_rows_cover_exactly():
             for a, b in zip(spans, spans[1:]):
                 assert a[1] == b[0]
             assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+
+
+def test_predicted_speedup_model():
+    """The strong-scaling model bench.py reports for config 3: the scatter
+    divides over the ranks, FFT + image do not, one reduce per call."""
+    from ska_sdp_func.grid_data.distributed import (predicted_speedup,
+                                                    reduce_ms_model)
+
+    assert reduce_ms_model(1 << 29, 1) == 0.0
+    # Ring reduce: (N - 1) / N of the buffer over the bus bandwidth.
+    assert abs(reduce_ms_model(3e11, 4, bus_gbs=300.0) - 750.0) < 1e-9
+    one = predicted_speedup(40.0, 0.4, 1, 1 << 29, 1 << 27)
+    assert one["grid"]["speedup"] == 1.0 and one["image"]["speedup"] == 1.0
+    p = predicted_speedup(40.0, 0.4, 8, 1 << 29, 1 << 27)
+    # The image reduce moves 4x fewer bytes than the grid reduce.
+    assert p["image"]["speedup"] > p["grid"]["speedup"] > 1.0
+    assert p["image"]["speedup"] < 8.0
+    m = predicted_speedup(40.0, 0.4, 8, 1 << 29, 1 << 27,
+                          reduce_ms={"grid": 2.0})
+    assert m["grid"]["reduce"] == "measured"
+    assert abs(m["grid"]["ms"] - (5.0 + 2.0 + 0.4)) < 1e-9
