@@ -6,7 +6,9 @@ determine_max_w_tower_height, w spread over 32 w-stack planes.
 
 A "step" is one wstack_wtower_grid_all over all rows. With --gpus N (one
 process per GPU, torchrun), the w-stack planes are sharded across the ranks
-(grid_planes with plane_offset = rank, plane_stride = N) and the rank
+(grid_plane_set with the planes assigned by a cost model: visibilities per
+plane + a fixed image-side cost, heaviest plane to the least-loaded rank;
+ska_sdp_func.grid_data.distributed.assign_planes) and the rank
 images are summed on rank 0 with one RCCL reduce inside the timed region;
 total work is fixed ("scaling": "strong"). Inputs are generated in HBM
 (uvw f32, vis c64, f0 = c so that metres are wavelengths).
@@ -29,6 +31,10 @@ sys.path.insert(0, ROOT)
 C_0 = 299792458.0
 F32_PEAK_TFLOPS = 157.3
 KW = dict(support=8, oversampling=16384, w_support=8, w_oversampling=16384)
+# Image-side cost of one w-stack plane (plane FFT, cut-out / update, grid
+# gather) in units of the mean plane's visibility load: ~8 ms against
+# ~20 ms of towers per plane at config 4 (profiles/r4_wtower_kernel_stats).
+PLANE_FIXED = 0.4
 
 
 def parse():
@@ -190,9 +196,21 @@ def main():
               KW["support"], KW["oversampling"], KW["w_support"],
               KW["w_oversampling"], 0.0, H)
 
+    # Multi-GPU: the w-stack planes are dealt to the ranks by a cost model
+    # (visibilities per plane + a fixed image-side cost per plane, longest
+    # first to the least-loaded rank), outside the timed region.
+    from ska_sdp_func.grid_data.distributed import (assign_planes,
+                                                    plane_balance,
+                                                    wstack_plane_loads)
+    first, loads = wstack_plane_loads(uvw, C_0, C_0 / 200, args.chan, w_step,
+                                      H)
+    masks, pcost = assign_planes(loads, world,
+                                 fixed_cost=PLANE_FIXED * loads.mean())
+    my_mask = torch.from_numpy(masks[rank]).to(dev)
+
     def grid_step(verbosity=0):
-        g.wstack_wtower_grid_planes(vis, *common, verbosity, image, rank,
-                                    world)
+        g.wstack_wtower_grid_plane_set(vis, *common, verbosity, image, first,
+                                       my_mask)
         if dist is not None:
             dist.reduce(image, dst=0)
 
@@ -233,17 +251,18 @@ def main():
     if args.degrid:
         out = torch.zeros_like(vis)
         for _ in range(args.warmup):
-            g.wstack_wtower_degrid_planes(image, *common, 0, out, rank,
-                                          world)
+            g.wstack_wtower_degrid_plane_set(image, *common, 0, out, first,
+                                             my_mask)
         barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            g.wstack_wtower_degrid_planes(image, *common, 0, out, rank,
-                                          world)
+            g.wstack_wtower_degrid_plane_set(image, *common, 0, out, first,
+                                             my_mask)
         barrier()
         t_deg = time.perf_counter() - t0
         g.wstack_wtower_enable_timing(True)
-        g.wstack_wtower_degrid_planes(image, *common, 0, out, rank, world)
+        g.wstack_wtower_degrid_plane_set(image, *common, 0, out, first,
+                                         my_mask)
         barrier()
         droof = roofline(g.wstack_wtower_get_timing(), "k_tower_idft")
         g.wstack_wtower_enable_timing(False)
@@ -281,6 +300,7 @@ def main():
                 "theta": theta, "fov": fov, "w_step": w_step,
                 "w_tower_height": H,
                 "parallelism": f"w-stack planes / {world}",
+                "plane_balance": round(plane_balance(pcost), 4),
             },
             "roofline": roof,
             "degrid": degrid,

@@ -24,6 +24,8 @@
 #ifndef SDP_GRID_WSTACK_WTOWER_H_
 #define SDP_GRID_WSTACK_WTOWER_H_
 
+#include <stdint.h>
+
 #include "ska-sdp-func/utility/sdp_mem.h"
 
 #ifdef __cplusplus
@@ -128,6 +130,60 @@ void sdp_grid_wstack_wtower_degrid_planes(
         sdp_Mem* vis,
         int plane_offset,
         int plane_stride,
+        sdp_Error* status
+);
+
+/* MI355X extension: the same operations restricted to an explicit set of
+ * w-stack planes, for load-balanced sharding across GPUs. Plane iw is the
+ * reference's w-stack plane index (w f / c in [iw d - d/2, (iw + 1) d -
+ * d/2), d = w_tower_height * w_step, sdp_grid_wstack_wtower.cpp:336-343);
+ * it is processed iff plane_first <= iw < plane_first + n and
+ * plane_mask[iw - plane_first] != 0, plane_mask a 1-D int32 array of n
+ * entries (host or device). Disjoint masks covering every plane give images
+ * / visibilities that sum to the grid_all / degrid_all ones. */
+void sdp_grid_wstack_wtower_grid_plane_set(
+        const sdp_Mem* vis,
+        double freq0_hz,
+        double dfreq_hz,
+        const sdp_Mem* uvw,
+        int subgrid_size,
+        double theta,
+        double w_step,
+        double shear_u,
+        double shear_v,
+        int support,
+        int oversampling,
+        int w_support,
+        int w_oversampling,
+        double subgrid_frac,
+        double w_tower_height,
+        int verbosity,
+        sdp_Mem* image,
+        int64_t plane_first,
+        const sdp_Mem* plane_mask,
+        sdp_Error* status
+);
+
+void sdp_grid_wstack_wtower_degrid_plane_set(
+        const sdp_Mem* image,
+        double freq0_hz,
+        double dfreq_hz,
+        const sdp_Mem* uvw,
+        int subgrid_size,
+        double theta,
+        double w_step,
+        double shear_u,
+        double shear_v,
+        int support,
+        int oversampling,
+        int w_support,
+        int w_oversampling,
+        double subgrid_frac,
+        double w_tower_height,
+        int verbosity,
+        sdp_Mem* vis,
+        int64_t plane_first,
+        const sdp_Mem* plane_mask,
         sdp_Error* status
 );
 

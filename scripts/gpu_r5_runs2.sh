@@ -1,0 +1,9 @@
+#!/bin/bash
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=${1:-gpurun_out/r5runs2}
+mkdir -p "$OUT"
+timeout -k 10 600 python -u -m pytest tests/test_es_runs_gpu.py -x -q --timeout 300 --timeout-method thread \
+    > "$OUT/pytest.log" 2>&1 || { tail -40 "$OUT/pytest.log"; exit 1; }
+tail -2 "$OUT/pytest.log"
+scripts/ab_c3.sh "$OUT/ab" 2 "ska-sdp-func_amd variants/c128 variants/base" || exit 1

@@ -30,12 +30,8 @@
 // values it adds to held across the transform) spills at 4 (image phase
 // 0.32 ms); loading those values after the transform instead (103 VGPRs,
 // 4-5 waves) measured 0.164-0.175 ms.
-#ifndef SDP_COLA_WAVES
 #define SDP_COLA_WAVES 4
-#endif
-#ifndef SDP_COLB_WAVES
 #define SDP_COLB_WAVES 3
-#endif
 
 namespace sdp_es {
 namespace {
@@ -702,8 +698,10 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
             float val;
             if constexpr (DO_W)
             {
-                float re, im;
-                phasor(ip, plane, abs(xo), abs(yo), -1.0f, re, im);
+                // Only the image rows need the w-screen (a third of the
+                // padded rows are cropped; rows are wave-uniform).
+                float re = 0.0f, im = 0.0f;
+                if (in) phasor(ip, plane, abs(xo), abs(yo), -1.0f, re, im);
                 val = x.x * re - x.y * im;
             }
             else
@@ -746,13 +744,10 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
 // (config 2) 32 x 128 beat 64 x 64 and 128 x 32 (A/B: gridding FFT 0.288
 // -> 0.259 ms, degridding image pass 0.113 -> 0.090 ms): the strided pass
 // then runs 128-point columns over rows 32 apart.
-#ifndef SDP_HALF_N1
-#define SDP_HALF_N1 32
-#endif
 template<int G2> struct HalfSplit;
 template<> struct HalfSplit<1024> { static constexpr int N1 = 32, N2 = 32; };
 template<> struct HalfSplit<2048> { static constexpr int N1 = 32, N2 = 64; };
-template<> struct HalfSplit<4096> { static constexpr int N1 = SDP_HALF_N1, N2 = 4096 / SDP_HALF_N1; };
+template<> struct HalfSplit<4096> { static constexpr int N1 = 32, N2 = 128; };
 
 // Occupancy of the row pass's loads. With P = G / 16 threads per row and
 // 16 elements each, thread p's element r of a row sits at column p + r P
@@ -803,83 +798,7 @@ __global__ void __launch_bounds__(320) k_row_occupancy(
         occ[tu * (S + 1) + cls] = (uint32_t)(m >> (t & 32));
 }
 
-// The two H rows of a quad are transformed side by side by the two halves
-// of the workgroup (each its own LDS row buffer), then swapped through LDS:
-// half 0 writes Z[k], half 1 Z[G/2 - k], both as (own + conj(other)) +
-// i (own - conj(other)) w with w = e^{2 pi i k / G}, resp.
-// e^{2 pi i (G/2 - k) / G} (one workgroup holding both rows' results in
-// registers needed 252 VGPRs, one workgroup per CU).
-template<int G>
-__global__ void __launch_bounds__(2 * RowPlan<G>::P)
-k_rows_herm(float2* __restrict__ grid, int k0, int M,
-        const float2* __restrict__ W, const uint32_t* __restrict__ occ)
-{
-    using F = RowFft<G, 1>;
-    constexpr int P = RowPlan<G>::P, EPT = F::EPT;
-    constexpr int NC = occ_classes(G), NQ = G / 4 + 1;
-    static_assert(EPT == 16 && P == G / 16 && P % 64 == 0,
-            "element r of thread p at column p + r P (k_row_occupancy)");
-    constexpr int kRowLds = G + G / 16;            // float2 per row buffer
-    extern __shared__ float2 lds[];
-    const int half = threadIdx.x / P;              // wave-uniform
-    const int p = threadIdx.x - half * P;
-    float2* my_lds = lds + half * kRowLds;
-    const float2* other_lds = lds + (1 - half) * kRowLds;
-    const Buf gb(grid - k0, grid_bytes(G, k0));
-    F f;
-    f.init(p, W, G);
-    const int per = (NQ + gridDim.x - 1) / gridDim.x;
-    const int q_begin = blockIdx.x * per, q_end = min(NQ, q_begin + per);
-    for (int k = q_begin; k < q_end; ++k)
-    {
-        const int pq = opaque(p);
-        // H row u from grid rows u and -u (elements v and -v); tiles with
-        // no bucketed entry were not written by the scatter: read as zero.
-        const int u = half ? G / 2 - k : k;        // k = G/4: both the same
-        const int ur = (G - u) & (G - 1);
-        const uint32_t oa_bits = occ ?
-                occ[(u >> 6) * NC + (pq >> 6)] : 0xFFFFFFFFu;
-        const uint32_t ob_bits = occ ?
-                occ[(ur >> 6) * NC + ((pq + 63) >> 6)] >> 16 : 0xFFFFFFFFu;
-        const uint32_t ra = ((uint32_t)u * G + k0) * 8u;
-        const uint32_t rb = ((uint32_t)ur * G + k0) * 8u;
-        float2 v[EPT];
-        F::load_input(v, [&](int c) {
-            const int ca = pq + c, cb = (G - ca) & (G - 1);
-            const bool oa = (oa_bits >> (c / P)) & 1u;
-            const bool ob = (ob_bits >> (c / P)) & 1u;
-            const float2 a = gb.load_if(oa, ra + (uint32_t)ca * 8u);
-            const float2 b = gb.load_if(ob, rb + (uint32_t)cb * 8u);
-            return make_float2(0.5f * (a.x + b.x), 0.5f * (a.y - b.y));
-        });
-        f.transform(v, pq, my_lds, RowIdx{});
-        // Swap the two halves' results (same thread layout in both).
-        __syncthreads();
-        F::store_output(v, [&](int c, int, float2 x) {
-            my_lds[RowIdx::off(pq + c)] = x;
-        });
-        __syncthreads();
-        // e^{2 pi i k / G} = conj(W[k]); e^{2 pi i (G/2 - k) / G} = -W[k].
-        const float2 wt = W[k];
-        const float2 w = half ? make_float2(-wt.x, -wt.y)
-                              : make_float2(wt.x, -wt.y);
-        F::store_output(v, [&](int c, int i, float2 a) {
-            const float2 b = other_lds[RowIdx::off(pq + c)];
-            const float2 xe = make_float2(a.x + b.x, a.y - b.y);
-            const float2 xo = cmul(make_float2(a.x - b.x, a.y + b.y), w);
-            v[i] = make_float2(xe.x - xo.y, xe.y + xo.x);
-        });
-        // Half 0: Z row k; half 1: Z row G/2 - k (not for k = 0, G/4).
-        const bool write = !half || (k > 0 && 2 * k < G / 2);
-        const uint32_t vr = (uint32_t)u * G * 8u + (uint32_t)pq * 8u;
-        F::store_output(v, [&](int c, int, float2 x) {
-            gb.store_if(write && (unsigned)(pq + c - k0) < (unsigned)M, x,
-                    vr + c * 8u);
-        });
-    }
-}
-
-// Single-row form of the real-output row pass (SDP_ES_HERM_ROWS=1): one
+// Single-row form of the real-output row pass: one
 // H row per iteration, H[u] = (A[u] + conj A[-u](-v)) / 2 for u = 0 .. G/2,
 // transformed and written as Bh[u] (M centre columns) into grid row u. A
 // workgroup is one row's threads and LDS (RowPlan<G>), so two share a CU and
@@ -944,15 +863,12 @@ k_rows_herm1(float2* __restrict__ grid, int k0, int M,
 // 15 - r). Workgroup 0 (class 0: element n2 pairs with N2 - n2, element 0
 // with Bh[G/2]) and workgroup N1/2 (class N1/2 with itself) load their
 // partners a second time and transform one class.
-#ifndef SDP_PAIRS_WAVES
+// Two waves per SIMD (3 measured 118 vs 110 us). 256 threads per
+// workgroup = 32 columns of 8 threads (256-byte row segments); 512 (64
+// columns, 512-byte segments) measured 110.9 -> 112.4 us.
 #define SDP_PAIRS_WAVES 2
-#endif
-// Threads per workgroup of the paired column pass A: 256 = 32 columns of
-// 8 threads (256-byte row segments), 512 = 64 columns (512 bytes).
-#ifndef SDP_PAIRS_THREADS
-#define SDP_PAIRS_THREADS 256
-#endif
-template<int N1, int N2, int NTH = SDP_PAIRS_THREADS>
+constexpr int kPairsThreads = 256;
+template<int N1, int N2, int NTH = kPairsThreads>
 __global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(SDP_PAIRS_WAVES)))
 k_cols_a_herm_pairs(float2* __restrict__ grid, int M,
         const float2* __restrict__ W)
@@ -1034,45 +950,6 @@ k_cols_a_herm_pairs(float2* __restrict__ grid, int M,
                 if (ok) gb.store(cmul(x, fs), vb, so_b + e * kStep);
             });
         }
-    }
-}
-
-// Column pass A of the half-length transform: for u1 = blockIdx.x,
-// length-N2 FFTs over the Z rows u1 + N1 * n2 (row pitch G = 2 N1 N2),
-// times e^{2 pi i u1 k2 / (G/2)}, back into rows u1 + N1 * k2.
-template<int N1, int N2>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_COLA_WAVES)))
-k_cols_a_herm(float2* __restrict__ grid, int M, const float2* __restrict__ W)
-{
-    constexpr int G = 2 * N1 * N2, B = ColPlan<N2>::B;
-    using F = ColFft<N2, 1>;
-    extern __shared__ float2 lds[];
-    const int c = threadIdx.x % B, p = threadIdx.x / B;
-    const int u1 = blockIdx.x;
-    const Buf gb(grid, grid_bytes(G, 0));
-    F f;
-    f.init(p, W, G);
-    float2 fs[F::EPT];
-#pragma unroll
-    for (int i = 0; i < F::EPT; ++i)
-        fs[i] = F::twiddle(W, 2 * u1 * F::out_index(p, i));
-    const int ncb = (M + B - 1) / B;
-    const uint32_t so = (uint32_t)u1 * G * 8u;
-    constexpr uint32_t kStep = (uint32_t)N1 * G * 8u;
-    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
-    {
-        const int pq = opaque(p), cq = opaque(c);
-        const int col = cb * B + cq;
-        const bool ok = col < M;
-        const uint32_t vo = ((uint32_t)pq * N1 * G + col) * 8u;
-        float2 v[F::EPT];
-        F::load_input(v, [&](int e) {
-            return ok ? gb.load(vo, so + e * kStep) : make_float2(0.f, 0.f);
-        });
-        f.transform(v, pq, lds, ColIdx<B>{cq});
-        F::store_output(v, [&](int e, int i, float2 x) {
-            if (ok) gb.store(cmul(x, fs[i]), vo, so + e * kStep);
-        });
     }
 }
 
@@ -1250,8 +1127,9 @@ k_cols_a_image(float* __restrict__ dirty, int correct_in_place,
             }
             if ((ix + iy) & 1) val = -val;
             float pr = 1.0f, pi = 0.0f;
+            // The zero-padding rows (val = 0) need no w-screen.
             if constexpr (DO_W)
-                phasor(ip, plane, abs(xo), abs(yo), 1.0f, pr, pi);
+                if (in) phasor(ip, plane, abs(xo), abs(yo), 1.0f, pr, pi);
             return make_float2(pr * val, pi * val);
         });
         f.transform(v, pq, lds, ColIdx<B>{cq});
@@ -1446,44 +1324,8 @@ k_cols_a_image_herm(float* __restrict__ dirty, float2* __restrict__ grid,
     }
 }
 
-// Column pass B (forward) of the half-length transform: for k2 =
-// blockIdx.x, length-N1 FFTs over rows k2 + N2 n1, results back into rows
-// k2 + N2 k1 (natural order Z[k] in row k; row pitch G).
-template<int N1, int N2>
-__global__ void __launch_bounds__(256)
-k_cols_b_image_herm(float2* __restrict__ grid, int M,
-        const float2* __restrict__ W)
-{
-    constexpr int G = 2 * N1 * N2, B = ColPlan<N1>::B;
-    using F = ColFft<N1, -1>;
-    extern __shared__ float2 lds[];
-    const int c = threadIdx.x % B, p = threadIdx.x / B;
-    const int k2 = blockIdx.x;
-    const Buf gb(grid, grid_bytes(G, 0));
-    F f;
-    f.init(p, W, G);
-    const int ncb = (M + B - 1) / B;
-    const uint32_t so = (uint32_t)k2 * G * 8u;
-    constexpr uint32_t kStep = (uint32_t)N2 * G * 8u;
-    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
-    {
-        const int pq = opaque(p), cq = opaque(c);
-        const int col = cb * B + cq;
-        const bool ok = col < M;
-        const uint32_t vo = ((uint32_t)pq * N2 * G + col) * 8u;
-        float2 v[F::EPT];
-        F::load_input(v, [&](int e) {
-            return ok ? gb.load(vo, so + e * kStep) : make_float2(0.f, 0.f);
-        });
-        f.transform(v, pq, lds, ColIdx<B>{cq});
-        F::store_output(v, [&](int e, int, float2 x) {
-            if (ok) gb.store(x, vo, so + e * kStep);
-        });
-    }
-}
-
 // Column pass B (forward) of the half-length transform in the single-row
-// form (SDP_ES_HERM_ROWS=1): after the length-N1 transforms it recovers
+// form: after the length-N1 transforms it recovers
 // the column spectra X[k] = (Z[k] + conj Z[G/2 - k]) / 2 - i (Z[k] - conj
 // Z[G/2 - k]) e^{-2 pi i k / G} / 2 itself and writes X[k] into row k
 // (k in [0, G/2]; X[G/2] from Z[0]), so the row pass takes one row per
@@ -1495,9 +1337,6 @@ k_cols_b_image_herm(float2* __restrict__ grid, int M,
 // out_index(p, i)); the pairs meet in registers. Workgroup N2/2 (class
 // N2/2 with itself) transforms its class twice; workgroup 0 (class 0,
 // element k1 paired with N1 - k1 mod N1) exchanges through LDS.
-#ifndef SDP_PAIRS_WAVES
-#define SDP_PAIRS_WAVES 2
-#endif
 template<int N1, int N2>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_PAIRS_WAVES)))
 k_cols_b_image_herm_pairs(float2* __restrict__ grid, int M,
@@ -1633,74 +1472,6 @@ k_rows_image_herm1(float2* __restrict__ grid, int k0, int M,
     }
 }
 
-// Row pass (forward) of the real-input form: quads as k_rows_herm; half 0
-// forms X[k] (grid rows k and G - k), half 1 X[G/2 - k] (rows G/2 - k and
-// G/2 + k; for k = 0 the row G/2 alone, for k = G/4 nothing). Only the
-// tiles the gather reads are written (k_row_occupancy<true>).
-template<int G>
-__global__ void __launch_bounds__(2 * RowPlan<G>::P)
-k_rows_image_herm(float2* __restrict__ grid, int k0, int M,
-        const float2* __restrict__ W, const uint32_t* __restrict__ need)
-{
-    using F = RowFft<G, -1>;
-    constexpr int P = RowPlan<G>::P, EPT = F::EPT;
-    constexpr int NC = occ_classes(G), NQ = G / 4 + 1;
-    static_assert(EPT == 16 && P == G / 16 && P % 64 == 0,
-            "element r of thread p at column p + r P (k_row_occupancy)");
-    constexpr int kRowLds = G + G / 16;
-    extern __shared__ float2 lds[];
-    const int half = threadIdx.x / P;
-    const int p = threadIdx.x - half * P;
-    float2* my_lds = lds + half * kRowLds;
-    const float2* other_lds = lds + (1 - half) * kRowLds;
-    const Buf gb(grid - k0, grid_bytes(G, k0));
-    F f;
-    f.init(p, W, G);
-    const int per = (NQ + gridDim.x - 1) / gridDim.x;
-    const int q_begin = blockIdx.x * per, q_end = min(NQ, q_begin + per);
-    for (int k = q_begin; k < q_end; ++k)
-    {
-        const int pq = opaque(p);
-        const int u = half ? G / 2 - k : k;         // X row (k = G/4: same)
-        const int zr = u & (G / 2 - 1);             // Z[G/2] = Z[0]
-        float2 v[EPT];
-        const uint32_t vz = (uint32_t)zr * G * 8u + (uint32_t)pq * 8u;
-        F::load_input(v, [&](int c) {
-            return gb.load_if((unsigned)(pq + c - k0) < (unsigned)M, vz + c * 8u);
-        });
-        // Swap the Z rows between the halves (input slot r = column p + r P).
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < EPT; ++r) my_lds[RowIdx::off(pq + r * P)] = v[r];
-        __syncthreads();
-        // e^{-2 pi i k / G} = W[k]; e^{-2 pi i (G/2 - k) / G} = -conj(W[k]).
-        const float2 wt = W[k];
-        const float2 w = half ? make_float2(-wt.x, wt.y) : wt;
-#pragma unroll
-        for (int r = 0; r < EPT; ++r)
-        {
-            const float2 a = v[r], b = other_lds[RowIdx::off(pq + r * P)];
-            const float2 dw = cmul(make_float2(a.x - b.x, a.y + b.y), w);
-            v[r] = make_float2(0.5f * ((a.x + b.x) + dw.y),
-                    0.5f * ((a.y - b.y) - dw.x));
-        }
-        f.transform(v, pq, my_lds, RowIdx{});
-        const bool write = !half || 2 * k != G / 2;
-        const int ur = (G - u) & (G - 1);
-        const uint32_t nf = need ? need[(u >> 6) * NC + (pq >> 6)] : ~0u;
-        const uint32_t nr = need ?
-                need[(ur >> 6) * NC + ((pq + 63) >> 6)] >> 16 : ~0u;
-        const uint32_t ro = ((uint32_t)u * G + k0) * 8u + (uint32_t)pq * 8u;
-        const uint32_t rr = ((uint32_t)ur * G + k0) * 8u;
-        F::store_output(v, [&](int c, int, float2 x) {
-            gb.store_if(write && ((nf >> (c / P)) & 1u), x, ro + c * 8u);
-            const int cr = (G - pq - c) & (G - 1);
-            gb.store_if(write && ur != u && ((nr >> (c / P)) & 1u),
-                    make_float2(x.x, -x.y), rr + (uint32_t)cr * 8u);
-        });
-    }
-}
-
 // Launch helpers --------------------------------------------------------------
 
 int num_cus()
@@ -1734,39 +1505,18 @@ int row_blocks(int G)
     return std::min(G, num_cus() * per_cu);
 }
 
-// Column-pass workgroups: rounds x the kernel's resident workgroups per CU
-// (env SDP_ES_COL_ROUNDS for experiments; default 2). A launch that is not
-// a whole number of resident rounds leaves its last round partly empty:
-// 4 per CU for the kernels that hold 3 (VGPRs) cost config 2 0.03 ms of
-// grid FFT + image and 0.05 ms of degrid FFT; the degrid column pass B
-// holds 5 (LDS) and ran 1.2 rounds at 6 per CU.
-int col_rounds()
-{
-    static int v = 0;
-    if (!v)
-    {
-        const char* e = getenv("SDP_ES_COL_ROUNDS");
-        v = e ? std::max(1, atoi(e)) : 2;
-    }
-    return v;
-}
-
-// The two paired column passes of the real-output form (k_cols_a_herm_pairs,
-// k_cols_b_image_herm_pairs: 2 resident per CU) run 4 rounds (env
-// SDP_ES_PAIR_ROUNDS): config 2, 110.7 -> 105.0 us and 97.6 -> 90.6 us
-// (rounds 1 / 3 / 8: 121.9 / 106.2 / 106.0 and 116.9 / 95.4 / 99.6 us;
-// the other column passes measured flat or slower past 2, except the 3-D
-// column pass B, which takes the same setting).
-int pair_rounds()
-{
-    static int v = 0;
-    if (!v)
-    {
-        const char* e = getenv("SDP_ES_PAIR_ROUNDS");
-        v = e ? std::max(1, atoi(e)) : 4;
-    }
-    return v;
-}
+// Column-pass workgroups: rounds x the kernel's resident workgroups per CU.
+// A launch that is not a whole number of resident rounds leaves its last
+// round partly empty: two rounds (4 per CU for the kernels that hold 3
+// (VGPRs) cost config 2 0.03 ms of grid FFT + image and 0.05 ms of degrid
+// FFT; the degrid column pass B holds 5 (LDS) and ran 1.2 rounds at 6 per
+// CU). The two paired column passes of the real-output form
+// (k_cols_a_herm_pairs, k_cols_b_image_herm_pairs: 2 resident per CU) and
+// the 3-D column pass B run four rounds: config 2, 110.7 -> 105.0 us and
+// 97.6 -> 90.6 us (rounds 1 / 3 / 8: 121.9 / 106.2 / 106.0 and 116.9 /
+// 95.4 / 99.6 us; the other column passes measured flat or slower past 2).
+constexpr int kColRounds = 2;
+constexpr int kPairRounds = 4;
 
 template<auto Kernel>
 dim3 col_grid(int fixed, int M, int B, int threads = 256,
@@ -1782,7 +1532,7 @@ dim3 col_grid(int fixed, int M, int B, int threads = 256,
         occ = n;
     }
     const int ncb = (M + B - 1) / B;
-    const int want = num_cus() * occ * (rounds > 0 ? rounds : col_rounds());
+    const int want = num_cus() * occ * (rounds > 0 ? rounds : kColRounds);
     const int split = std::max(1, std::min(ncb, (want + fixed - 1) / fixed));
     return dim3(fixed, split);
 }
@@ -1830,7 +1580,7 @@ int grid_to_image(const Geometry& g, const ImageParams<float>& ip, int plane,
     // 167.2 -> 160.5 us per plane; the 2-D form stays on col_rounds()).
     const dim3 blocks = ip.do_w ?
             col_grid<k_cols_b_grid<N1, N2, true>>(N2, g.M, ColPlan<N1>::B,
-                    256, kColLdsBytes, pair_rounds()) :
+                    256, kColLdsBytes, kPairRounds) :
             col_grid<k_cols_b_grid<N1, N2, false>>(N2, g.M, ColPlan<N1>::B);
     if (ip.do_w)
         k_cols_b_grid<N1, N2, true><<<blocks, 256, kColLdsBytes, stream>>>(
@@ -1843,45 +1593,17 @@ int grid_to_image(const Geometry& g, const ImageParams<float>& ip, int plane,
 }
 
 // Real-output (Hermitian) form of the 2-D gridding transform, for grids of
-// 2048 to 8192 (at 16384 the row pass's two 32-element rows per thread do
-// not fit the registers; env SDP_ES_HERM=0: the complex form, for A/B).
+// 2048 to 8192 (at 16384 the row pass's rows do not fit the registers; the
+// complex form serves 1024 and 16384, and every 3-D plane).
 bool herm_enabled(const ImageParams<float>& ip)
 {
-    static int on = -1;
-    if (on < 0)
-    {
-        const char* e = getenv("SDP_ES_HERM");
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
-    return on && !ip.do_w && ip.G >= 2048 && ip.G <= 8192;
+    return !ip.do_w && ip.G >= 2048 && ip.G <= 8192;
 }
 
-// The same for degridding (env SDP_ES_HERM_DEGRID=0: the complex form).
+// The same for degridding (real-input form).
 bool herm_degrid_enabled(const ImageParams<float>& ip)
 {
-    static int on = -1;
-    if (on < 0)
-    {
-        const char* e = getenv("SDP_ES_HERM_DEGRID");
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
-    return on && !ip.do_w && ip.G >= 2048 && ip.G <= 8192;
-}
-
-// Row passes of the real-output / real-input transforms in the single-row
-// form (k_rows_herm1 + k_cols_a_herm_pairs, k_cols_b_image_herm_pairs +
-// k_rows_image_herm1; the default: A/B at config 2, gridding row + column
-// pass 256 -> 242 us, degridding 236 -> 229 us) instead of row quads (env
-// SDP_ES_HERM_ROWS=0).
-bool herm_rows1()
-{
-    static int on = -1;
-    if (on < 0)
-    {
-        const char* e = getenv("SDP_ES_HERM_ROWS");
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
-    return on != 0;
+    return !ip.do_w && ip.G >= 2048 && ip.G <= 8192;
 }
 
 template<int N1, int N2>
@@ -1907,9 +1629,10 @@ int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
             SDP_HIP_CHECK_LAUNCH(&st);
             if (st) return st;
         }
-        if (herm_rows1())
         {
-            // One H row per workgroup iteration; Z formed in column pass A.
+            // One H row per workgroup iteration; Z formed in column pass A
+            // (single-row form; the row-quad form measured 256 -> 242 us
+            // for the row + column pass at config 2 and was removed).
             const size_t lds = row_lds_bytes(G);
             SDP_HIP_CHECK((allow_lds<k_rows_herm1<G>>(lds)), &st);
             if (st) return st;
@@ -1919,33 +1642,19 @@ int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
                     grid, g.k0, g.M, W, tiles ? occ : nullptr);
             SDP_HIP_CHECK_LAUNCH(&st);
             if (st) return st;
-            constexpr int kTh = SDP_PAIRS_THREADS;
+            constexpr int kTh = kPairsThreads;
             constexpr size_t kLds = kColLdsBytes * (kTh / 256);
             SDP_HIP_CHECK((allow_lds<k_cols_a_herm_pairs<HS::N1, HS::N2>>(
                     kLds)), &st);
             if (st) return st;
             const dim3 cg = col_grid<k_cols_a_herm_pairs<HS::N1, HS::N2>>(
                     HS::N1 / 2 + 1, g.M, kTh / ColPlan<HS::N2>::P, kTh, kLds,
-                    pair_rounds());
+                    kPairRounds);
             k_cols_a_herm_pairs<HS::N1, HS::N2><<<cg, kTh, kLds,
                     stream>>>(grid, g.M, W);
             SDP_HIP_CHECK_LAUNCH(&st);
             return st;
         }
-        const size_t lds = 2 * row_lds_bytes(G);
-        SDP_HIP_CHECK((allow_lds<k_rows_herm<G>>(lds)), &st);
-        if (st) return st;
-        const int blocks = std::min(G / 4 + 1, num_cus() *
-                (int)std::max<size_t>(1, (160 * 1024) / lds));
-        k_rows_herm<G><<<blocks, 2 * RowPlan<G>::P, lds, stream>>>(
-                grid, g.k0, g.M, W, tiles ? occ : nullptr);
-        SDP_HIP_CHECK_LAUNCH(&st);
-        if (st) return st;
-        k_cols_a_herm<HS::N1, HS::N2><<<col_grid<k_cols_a_herm<HS::N1,
-                HS::N2>>(HS::N1, g.M, ColPlan<HS::N2>::B), 256, kColLdsBytes,
-                stream>>>(grid, g.M, W);
-        SDP_HIP_CHECK_LAUNCH(&st);
-        return st;
     }
 }
 
@@ -2013,12 +1722,11 @@ int image_to_grid_herm(const Geometry& g, const float2* W, float2* grid,
             SDP_HIP_CHECK_LAUNCH(&st);
             if (st) return st;
         }
-        if (herm_rows1())
         {
             // X formed in column pass B; one row per workgroup iteration.
             const dim3 cg = col_grid<k_cols_b_image_herm_pairs<HS::N1,
                     HS::N2>>(HS::N2 / 2 + 1, g.M, ColPlan<HS::N1>::B, 256,
-                    kColLdsBytes, pair_rounds());
+                    kColLdsBytes, kPairRounds);
             k_cols_b_image_herm_pairs<HS::N1, HS::N2><<<cg, 256,
                     kColLdsBytes, stream>>>(grid, g.M, W);
             SDP_HIP_CHECK_LAUNCH(&st);
@@ -2033,20 +1741,6 @@ int image_to_grid_herm(const Geometry& g, const float2* W, float2* grid,
             SDP_HIP_CHECK_LAUNCH(&st);
             return st;
         }
-        k_cols_b_image_herm<HS::N1, HS::N2><<<col_grid<k_cols_b_image_herm<
-                HS::N1, HS::N2>>(HS::N2, g.M, ColPlan<HS::N1>::B), 256,
-                kColLdsBytes, stream>>>(grid, g.M, W);
-        SDP_HIP_CHECK_LAUNCH(&st);
-        if (st) return st;
-        const size_t lds = 2 * row_lds_bytes(G);
-        SDP_HIP_CHECK((allow_lds<k_rows_image_herm<G>>(lds)), &st);
-        if (st) return st;
-        const int blocks = std::min(G / 4 + 1, num_cus() *
-                (int)std::max<size_t>(1, (160 * 1024) / lds));
-        k_rows_image_herm<G><<<blocks, 2 * RowPlan<G>::P, lds, stream>>>(
-                grid, g.k0, g.M, W, tiles ? need : nullptr);
-        SDP_HIP_CHECK_LAUNCH(&st);
-        return st;
     }
 }
 

@@ -28,16 +28,23 @@ constexpr int kCoarseTile = kTile * kCoarse;   // 256 cells
 constexpr int kBinsPerPass = 16384;    // LDS histogram capacity (64 KiB)
 constexpr int kPiece = 4096;           // max entries per scatter work item
 constexpr int kMaxChunks = 1024;       // chunks of visibilities per bucketing
-#ifndef SDP_COUNT_CHUNKS
-#define SDP_COUNT_CHUNKS 2
-#endif
-constexpr int kCountChunks = SDP_COUNT_CHUNKS;   // chunks per counting
-                                                 // workgroup
+constexpr int kCountChunks = 2;        // chunks per counting workgroup
+                                       // (1: 62 / 47 us, 4: 67 / 46 us
+                                       // against 54 / 41 at config 2)
 constexpr int kGroupChunks = 16;       // chunks per level-2 group (and per
                                        // row of the tile count table)
 static_assert(kGroupChunks % kCountChunks == 0, "whole counting workgroups");
 constexpr int kMaxSuperBins = 1024;    // super bins (first bucketing level)
 constexpr int kMaxSuperTiles = 4096;   // tiles per super bin (S^2, S <= 64)
+// Channel runs (2-D f32 gridding with many channels): a row's channels move
+// radially through the uv plane and every tile sees them as one contiguous
+// run, so the records are runs (~4 channels each at config 3) instead of
+// visibilities (es_kernels.hip, "Channel runs").
+constexpr int kRunMinChan = 8;         // channels per row for the run path
+constexpr int kRunMaxChan = 65536;     // run lengths kept in 16 bits
+constexpr int kRunSeg = 8;             // channels per bucketing work unit
+constexpr int kRunWin = 128;           // runs staged per scatter window
+constexpr int kRunMapCap = 1024;       // entries per scatter window (bound)
 constexpr int kTapPolyPairs = 3;       // interior taps 1..6 of W = 8
 constexpr int kTapPolyDeg = 10;        // ~1e-9 relative (f32 Horner ~5e-7)
 
@@ -97,6 +104,14 @@ struct BucketScratch
     size_t recs_bytes = 0;
     size_t table_entries = 0;
     bool gtable_dirty = true;       // group rows not known to be zero
+    // Set by bucket(): the records are channel runs (pieces of <= kPiece
+    // runs), and the tile kernel reads the visibilities, weights and
+    // frequencies of the bucketed call itself.
+    bool runs = false;
+    int run_chan = 0;
+    const void* run_vis = nullptr;
+    const void* run_wt = nullptr;
+    float* inv_wl = nullptr;        // [kRunMaxChan]: per channel freq / c
 };
 
 // Number of visibility chunks used for a given visibility count and count
@@ -121,6 +136,10 @@ bool super_geometry(int ntiles, int* sshift, int* nsuper, int* nsbins);
 // plane p derive the tap (plane_tap) and skip the records off that plane.
 // Record layouts:
 //   grid, 2-D:  {pu, pv, vre*w, vim*w}
+//   grid, 2-D, f32, kRunMinChan <= channels <= kRunMaxChan (channel runs):
+//               {u, v, row * channels + first channel, (length - 1) |
+//               (tile inside its super bin) << 16}, one per (row, tile,
+//               maximal range of consecutive channels touching the tile)
 //   grid, 3-D:  {pu, pv, vre*w, vim*w*flip, pos_w, 0, 0, 0}
 //   degrid:     {pu, pv, flip (2-D) | pos_w*flip (3-D), index bits}
 template<typename T>
@@ -140,11 +159,9 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         bool accumulate = false);
 
 // Degrid-mode tile gather: vis[idx] += sum_taps grid * kernel.
-// sort_records: reorder each work item's records by sub-tile first (f32,
-// W <= 8; once per bucketing -- later planes of a 3-D call reuse the order).
 template<typename T>
 int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
-        const T* grid, T* vis, hipStream_t stream, bool sort_records = true);
+        const T* grid, T* vis, hipStream_t stream);
 
 // Image-plane kernels. image N x N (real), grid G x G complex (interleaved).
 // conv_corr: [N/2+1] normalised separable correction; quad_*: Gauss-Legendre

@@ -77,7 +77,6 @@ __device__ __forceinline__ void axis_taps(const EsParams<float>& p, float pos,
     using f2 = __attribute__((ext_vector_type(2))) float;
     const float hs = (float)p.support / 2.0f;
     const float inv_hs = 1.0f / hs;
-#ifndef SDP_AB_NO_TAP_POLY   // (A/B builds only: scripts/variant_lib.sh)
     if (POLY && NTAP == 9 && p.tap_poly_ok && u1 >= u0 + 7 &&
             u0 == (int)ceilf(pos - hs))
     {
@@ -105,7 +104,6 @@ __device__ __forceinline__ void axis_taps(const EsParams<float>& p, float pos,
                     ((float)(u0 + 8) - pos) * inv_hs);
         return;
     }
-#endif
 #pragma unroll
     for (int d = 0; d < NTAP; ++d)
     {
@@ -654,17 +652,12 @@ __device__ __forceinline__ void copy_rec(T* dst, const T* src)
 // bytes (1 of 32 or 64) per thread, so that the LDS stage of a 1024-thread
 // block stays below 80 KiB and two blocks share a CU (one block's loads
 // overlap the other's sort and stores).
-#ifndef SDP_FILL1_BYTES
-#define SDP_FILL1_BYTES 48
-#endif
-#ifndef SDP_FILL1_WAVES
-#define SDP_FILL1_WAVES 1   // blocks per CU (VGPR budget 128 / this)
-#endif
+constexpr int kFill1Bytes = 48;
 template<typename T, int W>
 struct Fill1Shape
 {
-    static constexpr int K = (SDP_FILL1_BYTES / (W * (int)sizeof(T))) > 0 ?
-            SDP_FILL1_BYTES / (W * (int)sizeof(T)) : 1;
+    static constexpr int K = (kFill1Bytes / (W * (int)sizeof(T))) > 0 ?
+            kFill1Bytes / (W * (int)sizeof(T)) : 1;
 };
 
 // First bucketing level: the chunk's records by super bin. A block walks
@@ -676,9 +669,11 @@ struct Fill1Shape
 // Record layouts as k_bucket_fill's were: see es_kernels.h. Positions in
 // a super bin follow the chunk order (scanned count-table columns), which
 // lets k_bucket_fill2 find the records of any chunk range.
+// One 1024-thread block per CU (VGPR budget 128; two blocks need <= 64
+// VGPRs and spill).
 template<typename T, int MODE, bool DO_W, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(
-        SDP_FILL1_WAVES * NT / 256))) void k_bucket_fill1(EsParams<T> p,
+        NT / 256))) void k_bucket_fill1(EsParams<T> p,
         int64_t num_rows, int num_chan, int64_t chunk, const T* __restrict__ uvw,
         const T* __restrict__ freq, const T* __restrict__ vis,
         const T* __restrict__ weight, const uint32_t* __restrict__ stable,
@@ -860,7 +855,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(
 // the tile of its first tap (degrid); tile f's records from these chunks
 // occupy [bin_start[f] + table[c0][f], ...), a window of a few hundred
 // bytes per tile that the block fills while it stays in L2.
-template<typename T, int MODE, bool DO_W>
+// RUNS: channel-run records (one tile each, its index inside the super bin
+// in the high half of word 3).
+template<typename T, int MODE, bool DO_W, bool RUNS = false>
 __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
         const uint32_t* __restrict__ stable,
         uint32_t* __restrict__ gtable,
@@ -920,6 +917,13 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
         for (int q = 0; q < kIn; ++q)
         {
             if (e + q * 256 >= e1) break;
+            if constexpr (RUNS)
+            {
+                const int j = (int)(__float_as_uint((float)rec[q][3]) >> 16);
+                const uint32_t pos = atomicAdd(&cur[j], 1u);
+                store_rec<T, kWords>(recs + (size_t)pos * kWords, rec[q]);
+                continue;
+            }
             int u0, u1, v0, v1, tu0, tu1, tv0, tv1;
             tap_range(p, rec[q][0], rec[q][1], u0, u1, v0, v1);
             tile_span<T, MODE>(p, u0, u1, v0, v1, tu0, tu1, tv0, tv1);
@@ -933,6 +937,256 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
                     store_rec<T, kWords>(recs + (size_t)pos * kWords, rec[q]);
                 }
         }
+    }
+}
+
+
+// Channel runs -------------------------------------------------------------
+//
+// 2-D f32 gridding with kRunMinChan <= C <= kRunMaxChan channels. The
+// channels of a row sit at u * f_c / c * uv_scale, moving radially with f_c,
+// so the channels whose support touches a given tile form contiguous runs
+// (exactly one per (row, tile) for monotonic frequencies; any order of
+// frequencies is handled, a run is a maximal range of consecutive channels).
+// A run is bucketed as ONE 16-byte record {u, v, first visibility index,
+// length - 1 | tile inside its super bin << 16}: ~18 records per row of 64
+// channels at config 3 instead of ~79 visibility records, and the tile
+// kernel reads the visibilities, weights and frequencies itself.
+//
+// Work units: (row, segment of kRunSeg channels). A unit owns the runs that
+// START in its segment and follows each to its end (possibly past the
+// segment), so no run is split. Spans and positions are footprint()'s
+// arithmetic (p.do_w == 0, flip 1).
+struct Span
+{
+    int tu0, tu1, tv0, tv1;     // tile span; empty: tu0 > tu1
+    __device__ bool has(int tu, int tv) const
+    {
+        return tu >= tu0 && tu <= tu1 && tv >= tv0 && tv <= tv1;
+    }
+};
+
+__device__ __forceinline__ Span empty_span()
+{
+    Span s;
+    s.tu0 = 1; s.tu1 = 0; s.tv0 = 1; s.tv1 = 0;
+    return s;
+}
+
+// Tiles touched by a channel of a row (grid mode, 2-D), from the channel's
+// inverse wavelength iwl = freq / c (k_inv_wavelength: the same quotient
+// footprint() forms with flip 1): footprint()'s positions and clamped tap
+// range, then tile_span().
+__device__ __forceinline__ Span chan_span(const EsParams<float>& p, float u,
+        float v, float iwl)
+{
+#pragma clang fp contract(off)
+    const float hs = (float)p.support / 2.0f;
+    const int gmin = -p.G / 2, gmax = (p.G - 1) / 2;
+    const float pu = u * iwl * p.uv_scale, pv = v * iwl * p.uv_scale;
+    const int u0 = max((int)ceilf(pu - hs), gmin);
+    const int u1 = min((int)floorf(pu + hs), gmax);
+    const int v0 = max((int)ceilf(pv - hs), gmin);
+    const int v1 = min((int)floorf(pv + hs), gmax);
+    if (u0 > u1 || v0 > v1) return empty_span();
+    Span s;
+    tile_span<float, MODE_GRID>(p, u0, u1, v0, v1, s.tu0, s.tu1, s.tv0,
+            s.tv1);
+    return s;
+}
+
+// Per channel: freq / c in f32, footprint()'s inverse wavelength (flip 1).
+__global__ void k_inv_wavelength(const float* __restrict__ freq, int n,
+        float* __restrict__ iwl)
+{
+#pragma clang fp contract(off)
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < n) iwl[c] = (1.0f * freq[c]) / (float)kSpeedOfLight;
+}
+
+__device__ __forceinline__ int super_of(const EsParams<float>& p, int tu,
+        int tv)
+{
+    return (tu >> p.sshift) * p.nsuper + (tv >> p.sshift);
+}
+
+__device__ __forceinline__ uint32_t tile_in_super(const EsParams<float>& p,
+        int tu, int tv)
+{
+    const int m = (1 << p.sshift) - 1;
+    return (uint32_t)(((tu & m) << p.sshift) | (tv & m));
+}
+
+// Run starts of segment [s0, s1): fn(tu, tv) for every (tile, channel) with
+// the tile in the channel's span and not in the previous channel's.
+template<typename F>
+__device__ __forceinline__ void run_starts(const EsParams<float>& p, float u,
+        float v, const float* __restrict__ iwl, int s0, int s1, F&& fn)
+{
+    Span prev = s0 > 0 ? chan_span(p, u, v, iwl[s0 - 1]) : empty_span();
+    for (int c = s0; c < s1; ++c)
+    {
+        const Span cur = chan_span(p, u, v, iwl[c]);
+        for (int tu = cur.tu0; tu <= cur.tu1; ++tu)
+            for (int tv = cur.tv0; tv <= cur.tv1; ++tv)
+                if (!prev.has(tu, tv)) fn(tu, tv);
+        prev = cur;
+    }
+}
+
+// The runs owned by segment [s0, s1) of a row of C channels, each followed
+// to its end: fn(tu, tv, first channel, length). At most 4 runs are open
+// (a support < 64 cells spans at most 2 x 2 tiles).
+template<typename F>
+__device__ __forceinline__ void run_walk(const EsParams<float>& p, float u,
+        float v, const float* __restrict__ iwl, int C, int s0, int s1,
+        F&& fn)
+{
+    Span prev = s0 > 0 ? chan_span(p, u, v, iwl[s0 - 1]) : empty_span();
+    int otu[4], otv[4], ost[4];
+    uint32_t live = 0;
+    for (int c = s0;; ++c)
+    {
+        const Span cur = c < C ? chan_span(p, u, v, iwl[c]) : empty_span();
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+        {
+            if (((live >> k) & 1u) && !cur.has(otu[k], otv[k]))
+            {
+                fn(otu[k], otv[k], ost[k], c - ost[k]);
+                live &= ~(1u << k);
+            }
+        }
+        if (c >= s1)
+        {
+            if (!live) break;
+            continue;
+        }
+        for (int tu = cur.tu0; tu <= cur.tu1; ++tu)
+            for (int tv = cur.tv0; tv <= cur.tv1; ++tv)
+            {
+                if (prev.has(tu, tv)) continue;
+                const int k = __builtin_ctz(~live);   // live has <= 3 bits
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                {
+                    if (q == k)
+                    {
+                        otu[q] = tu;
+                        otv[q] = tv;
+                        ost[q] = c;
+                    }
+                }
+                live |= 1u << k;
+            }
+        prev = cur;
+    }
+}
+
+// Counting pass of the run path: the k_bucket_count tables, counting runs
+// (a run is one record of one tile and its super bin).
+template<int NT>
+__global__ __launch_bounds__(NT) void k_bucket_count_runs(EsParams<float> p,
+        int64_t num_rows, int num_chan, int64_t chunk, int nc,
+        const float* __restrict__ uvw, const float* __restrict__ iwl,
+        uint32_t* __restrict__ stable, uint32_t* __restrict__ gtable)
+{
+    __shared__ uint32_t hist[kBinsPerPass];
+    __shared__ uint32_t shist[kCountChunks][kMaxSuperBins];
+    const int pass_base = blockIdx.y * kBinsPerPass;
+    const int nb = min(kBinsPerPass, p.nbins - pass_base);
+    const bool supers = blockIdx.y == 0;
+    for (int i = threadIdx.x; i < nb; i += NT) hist[i] = 0;
+    if (supers)
+        for (int i = threadIdx.x; i < kCountChunks * kMaxSuperBins; i += NT)
+            (&shist[0][0])[i] = 0;
+    __syncthreads();
+    const int nseg = (num_chan + kRunSeg - 1) / kRunSeg;
+    const int c_first = blockIdx.x * kCountChunks;
+#pragma unroll 1
+    for (int q = 0; q < kCountChunks; ++q)
+    {
+        const int64_t r0 = (int64_t)(c_first + q) * chunk;
+        const int64_t r1 = min(num_rows, r0 + chunk);
+        const uint32_t nunits = r1 > r0 ? (uint32_t)((r1 - r0) * nseg) : 0u;
+        uint32_t* sh = shist[q];
+        for (uint32_t unit = threadIdx.x; unit < nunits; unit += NT)
+        {
+            const uint32_t rl = unit / (uint32_t)nseg;
+            const int s0 = (int)(unit - rl * (uint32_t)nseg) * kRunSeg;
+            const int s1 = min(num_chan, s0 + kRunSeg);
+            const int64_t r = r0 + rl;
+            const float u = uvw[3 * r], v = uvw[3 * r + 1];
+            run_starts(p, u, v, iwl, s0, s1, [&](int tu, int tv) {
+                const int b = fine_bin(p, tu, tv) - pass_base;
+                if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
+                if (supers) atomicAdd(&sh[super_of(p, tu, tv)], 1u);
+            });
+        }
+    }
+    __syncthreads();
+    uint32_t* grow = gtable + (size_t)(c_first / kGroupChunks) * p.nbins +
+            pass_base;
+    for (int i = threadIdx.x; i < nb; i += NT)
+    {
+        const uint32_t n = hist[i];
+        if (n) atomicAdd(&grow[i], n);
+    }
+    if (supers)
+        for (int q = 0; q < kCountChunks && c_first + q < nc; ++q)
+        {
+            uint32_t* row = stable + (size_t)(c_first + q) * p.nsbins;
+            for (int i = threadIdx.x; i < p.nsbins; i += NT)
+                row[i] = shist[q][i];
+        }
+}
+
+// First level of the run path: a chunk's run records by super bin. One
+// thread walks one row's channels once (every row has the same channel
+// count, so the lanes of a wave walk in step) and stores each run at its
+// final position, the chunk's offset in the run's super bin (scanned count
+// table) plus a rank from an LDS atomic. The stores are scattered 16-byte
+// records, but ~4x fewer than visibility records.
+template<int NT>
+__global__ __launch_bounds__(NT) void k_bucket_fill1_runs(EsParams<float> p,
+        int64_t num_rows, int num_chan, int64_t chunk,
+        const float* __restrict__ uvw, const float* __restrict__ iwl,
+        const uint32_t* __restrict__ stable,
+        const uint32_t* __restrict__ bin_count, uint32_t* __restrict__ sb_start,
+        float* __restrict__ recs1)
+{
+    __shared__ uint32_t cursor[kMaxSuperBins];
+    __shared__ uint32_t loff[kMaxSuperBins];
+    __shared__ uint32_t s_wave[NT / 64];
+    const int t = threadIdx.x;
+    const int nsb = p.nsbins;
+    const uint32_t n_sb = block_scan_counts<NT>(bin_count + p.nbins, loff,
+            nsb, s_wave);
+    __syncthreads();
+    const uint32_t* row = stable + (size_t)blockIdx.x * p.nsbins;
+    for (int i = t; i < nsb; i += NT)
+    {
+        cursor[i] = loff[i] + row[i];
+        if (blockIdx.x == 0) sb_start[i] = loff[i];
+    }
+    if (blockIdx.x == 0 && t == 0) sb_start[nsb] = n_sb;
+    __syncthreads();
+    const int64_t r0 = (int64_t)blockIdx.x * chunk;
+    const int64_t r1 = min(num_rows, r0 + chunk);
+    float4* recs4 = (float4*)recs1;
+    for (int64_t r = r0 + t; r < r1; r += NT)
+    {
+        const float u = uvw[3 * r], v = uvw[3 * r + 1];
+        const uint32_t vbase = (uint32_t)(r * num_chan);
+        run_walk(p, u, v, iwl, num_chan, 0, num_chan,
+                [&](int tu, int tv, int c, int n) {
+            const int sb = super_of(p, tu, tv);
+            const uint32_t pos = atomicAdd(&cursor[sb], 1u);
+            recs4[pos] = make_float4(u, v,
+                    __uint_as_float(vbase + (uint32_t)c),
+                    __uint_as_float((uint32_t)(n - 1) |
+                            (tile_in_super(p, tu, tv) << 16)));
+        });
     }
 }
 
@@ -1284,29 +1538,61 @@ __device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
 // vector operations per operand. Barriers are LDS-only and the next
 // chunk's records load after this chunk's staging (no s_waitcnt vmcnt
 // before the visit loops).
-#ifndef SDP_SCATTER_VSTORE
-#define SDP_SCATTER_VSTORE 1
-#endif
 // Entries per chunk (<= 128: u taps staged by threads 0-127, v taps by
 // 128-255; 256: both axes per thread). The tap tables take 0.29 KB per
 // entry: 128 entries = 40 KB of LDS per workgroup (4 per CU), 96 = 30 KB (5).
-#ifndef SDP_SCATTER_NE
-#define SDP_SCATTER_NE 128
-#endif
-#ifndef SDP_SCATTER_WAVES
-#define SDP_SCATTER_WAVES 1
-#endif
-template<bool DO_W, int NTAP, int CHUNK = SDP_SCATTER_NE>
-__global__ __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsParams<float> p,
+constexpr int kScatterChunk = 128;
+// Inputs of the run path (channel runs, es_kernels.h): the bucketed call's
+// visibilities, weights and frequencies.
+struct RunSrc
+{
+    const float* vis;
+    const float* wt;
+    const float* inv_wl;    // per channel: freq / c, footprint()'s quotient
+    int chan;
+    uint32_t magic;         // floor(2^32 / chan): visibility index -> channel
+};
+
+// Exclusive scan of one value per thread over a 256-thread block; returns
+// the total. s_scan: 4 words of LDS; the caller synchronises before reusing
+// it.
+__device__ __forceinline__ uint32_t block_scan_256(uint32_t x, uint32_t& excl,
+        uint32_t* s_scan)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1)
+    {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_scan[wave] = inc;
+    lds_barrier();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+    {
+        const uint32_t y = s_scan[w];
+        before += w < wave ? y : 0u;
+        total += y;
+    }
+    excl = before + inc - x;
+    return total;
+}
+
+template<bool DO_W, int NTAP, int CHUNK = kScatterChunk, bool RUNS = false>
+__global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
         const uint32_t* __restrict__ item_bin, float* __restrict__ grid,
-        int flags)
+        int flags, RunSrc rs)
 {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     static_assert(CHUNK == 256 || (CHUNK <= 128 && CHUNK % 16 == 0),
             "one or two threads per entry");
+    static_assert(!RUNS || (!DO_W && CHUNK <= 128), "runs: 2-D, two threads "
+            "per entry");
     constexpr int kHalf = CHUNK == 256 ? 256 : 128;   // threads per axis
     constexpr int kVec = DO_W ? 2 : 1;
     constexpr int kStride = NTAP + 15;
@@ -1323,6 +1609,14 @@ __attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsPar
     // half and the v half of both are written by the entry's two threads.
     __shared__ uint32_t s_info[CHUNK];
     __shared__ uint32_t s_pos[CHUNK];
+    // Run path: the current window, up to kRunWin runs {u, v, first
+    // visibility index, first entry inside the window | first channel << 11}
+    // and the run of each of its <= kRunMap entries.
+    constexpr int kRunMap = RUNS ? (kRunMapCap / CHUNK) * CHUNK : 1;
+    static_assert(!RUNS || kRunMap < 2048, "11-bit window entry starts");
+    __shared__ float4 s_run[RUNS ? kRunWin : 1];
+    __shared__ uint8_t s_map[kRunMap];
+    __shared__ uint32_t s_scan[4];
 
     const uint32_t item = blockIdx.x;
     if (item_bin[item] == kNoBin) return;
@@ -1363,14 +1657,112 @@ __attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsPar
     }
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rw = r;
-    if (et < CHUNK && e0 + et < e1)
+    // Run path: entry e of the window = channel k of run j = s_map[e]; its
+    // inputs are loaded a chunk ahead (raw) and turned into the record
+    // {pu, pv, vre w, vim w} with footprint()'s arithmetic (the per-channel
+    // quotient freq / c from a table) when the chunk is staged.
+    float raw_u = 0.0f, raw_v = 0.0f, raw_iwl = 0.0f, raw_wt = 0.0f;
+    float2 raw_vis = make_float2(0.0f, 0.0f);
+    auto fetch = [&](uint32_t e) {
+        const float4 run = s_run[s_map[e]];
+        const uint32_t w = __float_as_uint(run.w);
+        const uint32_t k = e - (w & 0x7ffu);
+        const uint32_t vi = __float_as_uint(run.z) + k;
+        raw_u = run.x;
+        raw_v = run.y;
+        raw_iwl = rs.inv_wl[(w >> 11) + k];
+        if (stage_v)
+        {
+            raw_vis = *(const float2*)(rs.vis + 2 * (size_t)vi);
+            raw_wt = rs.wt[vi];
+        }
+    };
+    auto raw_rec = [&]() -> float4 {
+#pragma clang fp contract(off)
+        float4 q;
+        q.x = raw_u * raw_iwl * p.uv_scale;
+        q.y = raw_v * raw_iwl * p.uv_scale;
+        q.z = raw_vis.x * raw_wt;
+        q.w = raw_vis.y * raw_wt;
+        return q;
+    };
+    if (!RUNS && et < CHUNK && e0 + et < e1)
     {
         r = recs4[(size_t)(e0 + et) * kVec];
         if (DO_W) rw = recs4[(size_t)(e0 + et) * kVec + 1];
     }
-    for (uint32_t cb = e0; cb < e1; cb += CHUNK)
+    // Run path: windows of <= kRunMap entries (whole chunks) from <=
+    // kRunWin runs, the first possibly entered at an offset (a run longer
+    // than the window's room continues in the next one). One pass over
+    // [e0, e1) otherwise.
+    uint32_t wj = e0, wo = 0;       // window's first run, entry offset in it
+    for (bool more = e0 < e1; more;)
     {
-        const int n = (int)min((uint32_t)CHUNK, e1 - cb);
+    uint32_t c_end = e1, c_begin = e0;
+    more = false;
+    if (RUNS)
+    {
+        // s_run / s_map are free: every read of the previous window
+        // preceded its last B2 barrier.
+        const uint32_t nrun = min((uint32_t)kRunWin, e1 - wj);
+        float4 run = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        uint32_t len = 0;
+        if ((uint32_t)t < nrun)
+        {
+            run = recs4[wj + t];
+            const uint32_t off = t == 0 ? wo : 0u;
+            len = (__float_as_uint(run.w) & 0xffffu) + 1u - off;
+            const uint32_t vi = __float_as_uint(run.z) + off;
+            uint32_t q = __umulhi(vi, rs.magic);
+            if (vi - q * (uint32_t)rs.chan >= (uint32_t)rs.chan) ++q;
+            run.z = __uint_as_float(vi);
+            run.w = __uint_as_float((vi - q * (uint32_t)rs.chan) << 11);
+        }
+        uint32_t excl = 0;
+        const uint32_t tot = block_scan_256(len, excl, s_scan);
+        if ((uint32_t)t < nrun && excl < (uint32_t)kRunMap)
+        {
+            run.w = __uint_as_float(__float_as_uint(run.w) | excl);
+            s_run[t] = run;
+            const uint32_t hi = min(excl + len, (uint32_t)kRunMap);
+            for (uint32_t k = excl; k < hi; ++k) s_map[k] = (uint8_t)t;
+        }
+        lds_barrier();
+        c_begin = 0;
+        c_end = min(tot, (uint32_t)kRunMap);
+        // Next window: after the run holding the window's last entry, or
+        // inside it if it continues past the window.
+        if (tot > (uint32_t)kRunMap)
+        {
+            const uint32_t jl = s_map[kRunMap - 1];
+            const uint32_t ex = __float_as_uint(s_run[jl].w) & 0x7ffu;
+            const uint32_t ln = (jl == 0 ? wo : 0u) +
+                    (uint32_t)kRunMap - ex;   // entries of run jl consumed
+            const uint32_t full = (__float_as_uint(recs4[wj + jl].w) &
+                    0xffffu) + 1u;
+            if (ln < full)
+            {
+                wj += jl;
+                wo = ln;
+            }
+            else
+            {
+                wj += jl + 1;
+                wo = 0;
+            }
+        }
+        else
+        {
+            wj += nrun;
+            wo = 0;
+        }
+        more = wj < e1;
+        if (et < CHUNK && (uint32_t)et < c_end) fetch((uint32_t)et);
+    }
+    for (uint32_t cb = c_begin; cb < c_end; cb += CHUNK)
+    {
+        if (RUNS) r = raw_rec();
+        const int n = (int)min((uint32_t)CHUNK, c_end - cb);
         // Tap range of this thread's axis (both with CHUNK = 256): same
         // formula as tap_range / footprint.
         const float hs = (float)p.support / 2.0f;
@@ -1430,7 +1822,6 @@ __attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsPar
             {
                 float tu[NTAP];
                 axis_taps<NTAP, true>(p, r.x, u0, u1, tu);
-#if SDP_SCATTER_VSTORE
                 // 16-byte stores (eb is a multiple of 4): entry rows are
                 // kStride = 24 words apart, so a wave's one-word stores of
                 // tap d hit 8 banks (8-way conflicts); quads hit them 2-way.
@@ -1441,10 +1832,6 @@ __attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsPar
                             tu[d + 3]);
 #pragma unroll
                 for (int d = NTAP & ~3; d < NTAP; ++d) s_ku[eb + d] = tu[d];
-#else
-#pragma unroll
-                for (int d = 0; d < NTAP; ++d) s_ku[eb + d] = tu[d];
-#endif
             }
             if (stage_v)
             {
@@ -1452,7 +1839,6 @@ __attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsPar
                 axis_taps<NTAP, true>(p, r.y, v0, v1, tv);
                 const bool neg = ((u0 + v0) & 1) != 0;
                 const float zr = neg ? -r.z : r.z, zi = neg ? -r.w : r.w;
-#if SDP_SCATTER_VSTORE
                 float4* q = reinterpret_cast<float4*>(s_kv + eb);
 #pragma unroll
                 for (int d = 0; d + 2 <= NTAP; d += 2)
@@ -1461,21 +1847,24 @@ __attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsPar
                 if (NTAP & 1)
                     s_kv[eb + NTAP - 1] = make_float2(tv[NTAP - 1] * zr,
                             tv[NTAP - 1] * zi);
-#else
-#pragma unroll
-                for (int d = 0; d < NTAP; ++d)
-                    s_kv[eb + d] = make_float2(tv[d] * zr, tv[d] * zi);
-#endif
             }
         }
         // Next chunk's records, issued after this chunk's last use of r so
         // that nothing waits for them before the next staging.
-        if (et < CHUNK && cb + CHUNK + et < e1)
+        if (et < CHUNK && cb + CHUNK + et < c_end)
         {
-            r = recs4[(size_t)(cb + CHUNK + et) * kVec];
-            if (DO_W) rw = recs4[(size_t)(cb + CHUNK + et) * kVec + 1];
+            if (RUNS)
+            {
+                fetch(cb + CHUNK + et);
+            }
+            else
+            {
+                r = recs4[(size_t)(cb + CHUNK + et) * kVec];
+                if (DO_W) rw = recs4[(size_t)(cb + CHUNK + et) * kVec + 1];
+            }
         }
         lds_barrier();   // B2: entry words and tap tables complete
+
         uint32_t* list = s_list[wave];
         // The chunk's entry words, read once for the four column blocks.
         constexpr int kGroups = (CHUNK + 63) / 64;
@@ -1553,6 +1942,7 @@ __attribute__((amdgpu_waves_per_eu(SDP_SCATTER_WAVES))) void k_scatter_tab(EsPar
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
         }
     }
+    }   // windows
 #pragma unroll
     for (int cblk = 0; cblk < 4; ++cblk)
     {
@@ -1800,12 +2190,6 @@ __global__ __launch_bounds__(256) void k_gather_tab(EsParams<float> p,
 // ROWS: the tile rows one workgroup serves (64, or 32: each work item is
 // split over two workgroups by the row of the entries' first tap, so the
 // window is 40 x 72 and twice as many workgroups share a CU); NT threads.
-#ifndef SDP_WIN_STAGE_V2
-#define SDP_WIN_STAGE_V2 1
-#endif
-#ifndef SDP_WIN_CONTRACT_V2
-#define SDP_WIN_CONTRACT_V2 1
-#endif
 template<bool DO_W, int NTAP, int ROWS, int NT>
 __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
@@ -1840,7 +2224,6 @@ __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (e0 + t < e1) r = recs4[e0 + t];
-#if SDP_WIN_STAGE_V2
     // The window as 16-byte loads (two cells; c0 and G are even), all of a
     // thread's loads issued before the first LDS store: one memory latency
     // per work item instead of one per loop trip. Buffer loads relative to
@@ -1877,17 +2260,6 @@ __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
                 *reinterpret_cast<float4*>(&win[rr * kPitch + 2 * cq]) = wv[j];
         }
     }
-#else
-    const float2* g2 = (const float2*)grid;
-    for (int k = t; k < kWinR * kWin; k += NT)
-    {
-        const int rr = k / kWin, cc = k - rr * kWin;
-        float2 v = make_float2(0.0f, 0.0f);
-        if (rw0 + rr < p.G && c0 + cc < p.G)
-            v = g2[(size_t)(rw0 + rr) * p.G + c0 + cc];
-        win[rr * kPitch + cc] = v;
-    }
-#endif
     __syncthreads();
     for (uint32_t e = e0 + t; e < e1; e += NT)
     {
@@ -1908,7 +2280,7 @@ __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
         // 2-D: the unrolled form (92 VGPRs, 5 waves per SIMD) measured
         // 447 -> 438 us at config 2; 3-D (plane-tap divergence): the row
         // loop (70 VGPRs, 7 waves) 391 vs 403 us.
-        if constexpr (SDP_WIN_CONTRACT_V2 && !DO_W)
+        if constexpr (!DO_W)
         {
             // The ninth tap of an axis is non-zero only at an exact-integer
             // position (W + 1 taps, rare): the wave takes the 9 x 9 form
@@ -1975,114 +2347,6 @@ __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
         vis[2 * idx] += sr * ks;
         vis[2 * idx + 1] += si * ks * flip;
     }
-}
-
-// Degrid mode, ahead of k_gather_tab: each work item's records reordered
-// by the 16 x 16 sub-tile of their first tap (counting sort over the 16
-// keys, deterministic: key, then round, wave, lane), so that a chunk of
-// consecutive entries touches few of the 25 sub-tiles whose grid values the
-// gather loads (a chunk of unordered entries touches nearly all of them).
-// The piece is staged in LDS and written back in order, coalesced. Pieces
-// of more than kSortCap entries (hot tiles) are left as they are: the
-// small LDS footprint keeps 8 workgroups per CU on this memory-bound pass.
-constexpr int kSortCap = 1024;
-
-__global__ __launch_bounds__(256) void k_sort_pieces(EsParams<float> p,
-        float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
-        const uint32_t* __restrict__ item_start,
-        const uint32_t* __restrict__ item_bin)
-{
-    __shared__ float4 s_rec[kSortCap];
-    __shared__ uint16_t s_inv[kSortCap];     // slot -> entry
-    __shared__ uint32_t s_cnt[4][16];
-    __shared__ uint32_t s_run[16];
-    const uint32_t item = blockIdx.x;
-    if (item_bin[item] == kNoBin) return;
-    const int b = (int)item_bin[item];
-    const uint32_t piece = item - item_start[b];
-    const uint32_t e0 = bin_start[b] + piece * kPiece;
-    const uint32_t e1 = min(bin_start[b + 1], e0 + kPiece);
-    // One gather chunk: order is irrelevant; hot pieces: left unsorted.
-    if (e1 <= e0 + 256 || e1 > e0 + kSortCap) return;
-    const int n = (int)(e1 - e0);
-    const int half = p.G / 2;
-    int r0, c0;
-    tile_origin(p, b, r0, c0);
-    const int tu0 = r0 - half, tv0 = c0 - half;
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    float4* r4 = (float4*)recs;
-    for (int i = t; i < n; i += 256) s_rec[i] = r4[e0 + i];
-    __syncthreads();
-    auto key_of = [&](int i) -> int {
-        if (i >= n) return -1;
-        const float4 r = s_rec[i];
-        int u0, u1, v0, v1;
-        tap_range(p, r.x, r.y, u0, u1, v0, v1);
-        const int kr = min(max((u0 - tu0) >> 4, 0), 3);
-        const int kc = min(max((v0 - tv0) >> 4, 0), 3);
-        return kr * 4 + kc;
-    };
-    // Pass 1: per-key totals (lane k of each wave accumulates key k).
-    constexpr int kRounds = kSortCap / 256;
-    int keys[kRounds];
-#pragma unroll
-    for (int rd = 0; rd < kRounds; ++rd) keys[rd] = key_of(rd * 256 + t);
-    const int rounds = (n + 255) / 256;
-    uint32_t tot = 0;
-#pragma unroll
-    for (int rd = 0; rd < kRounds; ++rd)
-    {
-        if (rd >= rounds) break;
-        const int key = keys[rd];
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-        {
-            const uint64_t m = __ballot(key == k);
-            if (lane == k) tot += (uint32_t)__popcll(m);
-        }
-    }
-    if (lane < 16) s_cnt[wave][lane] = tot;
-    __syncthreads();
-    if (t == 0)
-    {
-        uint32_t run = 0;
-        for (int k = 0; k < 16; ++k)
-        {
-            s_run[k] = run;
-            run += s_cnt[0][k] + s_cnt[1][k] + s_cnt[2][k] + s_cnt[3][k];
-        }
-    }
-    __syncthreads();
-    // Pass 2: slots.
-#pragma unroll
-    for (int rd = 0; rd < kRounds; ++rd)
-    {
-        if (rd >= rounds) break;
-        const int i = rd * 256 + t;
-        const int key = keys[rd];
-        uint32_t c = 0, rk = 0;
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-        {
-            const uint64_t m = __ballot(key == k);
-            if (lane == k) c = (uint32_t)__popcll(m);
-            if (key == k) rk = (uint32_t)__popcll(m & lt);
-        }
-        if (lane < 16) s_cnt[wave][lane] = c;
-        __syncthreads();
-        if (key >= 0)
-        {
-            uint32_t pos = s_run[key] + rk;
-            for (int w = 0; w < wave; ++w) pos += s_cnt[w][key];
-            s_inv[pos] = (uint16_t)i;
-        }
-        __syncthreads();
-        if (t < 16)
-            s_run[t] += s_cnt[0][t] + s_cnt[1][t] + s_cnt[2][t] + s_cnt[3][t];
-        __syncthreads();
-    }
-    for (int j = t; j < n; j += 256) r4[e0 + j] = s_rec[s_inv[j]];
 }
 
 // Degrid mode: one workgroup per work item; the tile plus its support halo
@@ -2376,33 +2640,13 @@ void es_tap_poly_fit(double beta, float out[kTapPolyPairs]
     }
 }
 
-// Visibilities per bucketing chunk (env SDP_ES_CHUNK_VIS for experiments).
-int64_t chunk_vis()
-{
-    static int64_t v = 0;
-    if (!v)
-    {
-        const char* e = getenv("SDP_ES_CHUNK_VIS");
-        v = e ? std::max<int64_t>(256, atoll(e)) : 8192;
-    }
-    return v;
-}
-
-int bucket_threads()
-{
-    static int v = 0;
-    if (!v)
-    {
-        const char* e = getenv("SDP_ES_BUCKET_THREADS");
-        v = e ? atoi(e) : 1024;
-        if (v != 256 && v != 512 && v != 1024) v = 256;
-    }
-    return v;
-}
+// Visibilities per bucketing chunk: 8192 beat 12 k / 16 k / 32 k (fewer
+// blocks hurt both record levels).
+constexpr int64_t kChunkVis = 8192;
 
 int num_chunks(int64_t num_vis, int tstride)
 {
-    const int64_t cv = chunk_vis();
+    const int64_t cv = kChunkVis;
     const int64_t by_size = (num_vis + cv - 1) / cv;
     const int64_t by_table = (((int64_t)1 << 31) - 1) /
             (4 * (int64_t)std::max(1, tstride));
@@ -2460,14 +2704,6 @@ void launch_fill(int nc, int64_t chunk, const EsParams<T>& p,
             (const T*)s->recs1, (T*)s->recs);
 }
 
-#define SDP_ES_BY_THREADS(NTV, CALL) \
-    switch (NTV) \
-    { \
-    case 1024: { constexpr int NT = 1024; CALL; break; } \
-    case 512:  { constexpr int NT = 512;  CALL; break; } \
-    default:   { constexpr int NT = 256;  CALL; break; } \
-    }
-
 template<typename T>
 int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
         const T* uvw, const T* freq, const T* vis, const T* weight,
@@ -2493,7 +2729,13 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
     uint32_t* gtable = s->table;                                   // [ng][nbins]
     uint32_t* stable = s->table + s->table_entries -
             (size_t)nc * p.nsbins;                                 // [nc][nsbins]
-    const int nt = bucket_threads();
+    // Channel runs (2-D f32 gridding with many channels): run records.
+    const bool runs = sizeof(T) == 4 && mode == MODE_GRID && !p.do_w &&
+            num_chan >= kRunMinChan && num_chan <= kRunMaxChan;
+    s->runs = runs;
+    s->run_chan = num_chan;
+    s->run_vis = vis;
+    s->run_wt = weight;
     if (p.nsbins < 1 || p.nsbins > kMaxSuperBins ||
             (1 << (2 * p.sshift)) > kMaxSuperTiles ||
             p.tstride != p.nbins + p.nsbins ||
@@ -2509,14 +2751,31 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
                 sizeof(uint32_t), stream), status);
     if (*status) return *status;
     s->gtable_dirty = true;
-    if (mode == MODE_GRID)
-        SDP_ES_BY_THREADS(nt, (launch_count<T, MODE_GRID, NT>(grid_b, p,
-                num_rows, num_chan, chunk, nc, uvw, freq, stable, gtable,
-                stream)))
+    if constexpr (sizeof(T) == 4)
+    {
+        if (runs)
+        {
+            if (!s->inv_wl)
+            {
+                SDP_LOG_ERROR("Bucketing scratch has no channel table");
+                return SDP_ERR_RUNTIME;
+            }
+            k_inv_wavelength<<<(num_chan + 255) / 256, 256, 0, stream>>>(
+                    freq, num_chan, s->inv_wl);
+            k_bucket_count_runs<1024><<<grid_b, 1024, 0, stream>>>(p,
+                    num_rows, num_chan, chunk, nc, uvw, s->inv_wl, stable,
+                    gtable);
+            SDP_HIP_CHECK_LAUNCH(status);
+        }
+    }
+    if (runs)
+        ;
+    else if (mode == MODE_GRID)
+        launch_count<T, MODE_GRID, 1024>(grid_b, p, num_rows, num_chan,
+                chunk, nc, uvw, freq, stable, gtable, stream);
     else
-        SDP_ES_BY_THREADS(nt, (launch_count<T, MODE_DEGRID, NT>(grid_b, p,
-                num_rows, num_chan, chunk, nc, uvw, freq, stable, gtable,
-                stream)))
+        launch_count<T, MODE_DEGRID, 1024>(grid_b, p, num_rows, num_chan,
+                chunk, nc, uvw, freq, stable, gtable, stream);
     SDP_HIP_CHECK_LAUNCH(status);
     // Column prefixes (in place) and totals: tile counts over the chunk
     // groups into bin_count[0, nbins), super-bin counts over the chunks
@@ -2542,22 +2801,36 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
     }
     *n_entries = 0;                  // not known on the host
     *n_items = s->item_capacity;     // upper bound; extra items exit
-    if (mode == MODE_GRID)
+    if constexpr (sizeof(T) == 4)
+    {
+        if (runs)
+        {
+            k_bucket_fill1_runs<1024><<<nc, 1024, 0, stream>>>(p, num_rows,
+                    num_chan, chunk, uvw, s->inv_wl, stable, s->bin_count,
+                    s->sb_start, (float*)s->recs1);
+            k_bucket_fill2<float, MODE_GRID, false, true><<<dim3(ng,
+                    p.nsbins), 256, 0, stream>>>(p, nc, stable, gtable,
+                    s->bin_count, s->bin_start, s->sb_start,
+                    (const float*)s->recs1, (float*)s->recs);
+        }
+    }
+    if (runs)
+        ;
+    else if (mode == MODE_GRID)
     {
         if (p.do_w)
-            SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_GRID, true, NT>(nc,
-                    chunk, p, num_rows, num_chan, uvw, freq, vis, weight, s,
-                    stable, gtable, stream)))
+            launch_fill<T, MODE_GRID, true, 1024>(nc, chunk, p, num_rows,
+                    num_chan, uvw, freq, vis, weight, s, stable, gtable,
+                    stream);
         else
-            SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_GRID, false, NT>(nc,
-                    chunk, p, num_rows, num_chan, uvw, freq, vis, weight, s,
-                    stable, gtable, stream)))
+            launch_fill<T, MODE_GRID, false, 1024>(nc, chunk, p, num_rows,
+                    num_chan, uvw, freq, vis, weight, s, stable, gtable,
+                    stream);
     }
     else
     {
-        SDP_ES_BY_THREADS(nt, (launch_fill<T, MODE_DEGRID, false, NT>(nc,
-                chunk, p, num_rows, num_chan, uvw, freq, vis, weight, s,
-                stable, gtable, stream)))
+        launch_fill<T, MODE_DEGRID, false, 1024>(nc, chunk, p, num_rows,
+                num_chan, uvw, freq, vis, weight, s, stable, gtable, stream);
     }
     SDP_HIP_CHECK_LAUNCH(status);
     if (!*status) s->gtable_dirty = false;
@@ -2584,24 +2857,44 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     {
         const float* recs = (const float*)s.recs;
         const int se = (skip_empty ? 1 : 0) | (accumulate ? 2 : 0);
+        RunSrc rs = {};
+        if (s.runs)
+        {
+            rs.vis = (const float*)s.run_vis;
+            rs.wt = (const float*)s.run_wt;
+            rs.inv_wl = s.inv_wl;
+            rs.chan = s.run_chan;
+            rs.magic = (uint32_t)(0x100000000ull / (uint64_t)s.run_chan);
+        }
         if (p.support <= 16)
         {
-            if (p.support <= 8 && p.do_w)
+#ifndef SDP_RUNS_CHUNK
+#define SDP_RUNS_CHUNK 112
+#endif
+            if (s.runs && p.support <= 8)
+                k_scatter_tab<false, 9, SDP_RUNS_CHUNK, true><<<n_items, 256, 0,
+                        stream>>>(p, recs, s.bin_start, s.item_start,
+                        s.item_bin, grid, se, rs);
+            else if (s.runs)
+                k_scatter_tab<false, 17, 128, true><<<n_items, 256, 0,
+                        stream>>>(p, recs, s.bin_start, s.item_start,
+                        s.item_bin, grid, se, rs);
+            else if (p.support <= 8 && p.do_w)
                 k_scatter_tab<true, 9><<<n_items, 256, 0, stream>>>(
                         p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                        se);
+                        se, rs);
             else if (p.support <= 8)
                 k_scatter_tab<false, 9><<<n_items, 256, 0, stream>>>(
                         p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                        se);
+                        se, rs);
             else if (p.do_w)
                 k_scatter_tab<true, 17><<<n_items, 256, 0, stream>>>(
                         p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                        se);
+                        se, rs);
             else
                 k_scatter_tab<false, 17><<<n_items, 256, 0, stream>>>(
                         p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                        se);
+                        se, rs);
             SDP_HIP_CHECK_LAUNCH(status);
             return *status;
         }
@@ -2625,36 +2918,11 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     return *status;
 }
 
-// f32 gather form for W <= 8: 0 = lane-per-entry window (k_gather_win,
-// default), 1 = matrix-core sub-tile form (k_gather_tab; env
-// SDP_ES_GATHER=mfma).
-int gather_form()
-{
-    static int v = -1;
-    if (v < 0)
-    {
-        const char* e = getenv("SDP_ES_GATHER");
-        v = (e && strcmp(e, "mfma") == 0) ? 1 : 0;
-    }
-    return v;
-}
-
-// Degrid records sorted by first-tap sub-tile inside each work item before
-// k_gather_tab (env SDP_ES_SORT_PIECES=0 disables).
-bool sort_pieces()
-{
-    static int v = -1;
-    if (v < 0)
-    {
-        const char* e = getenv("SDP_ES_SORT_PIECES");
-        v = e ? atoi(e) : 1;
-    }
-    return v != 0;
-}
-
+// f32: W <= 8 the lane-per-entry window gather (k_gather_win), W = 16 the
+// matrix-core sub-tile form (k_gather_tab); f64: the LDS window gather.
 template<typename T>
 int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
-        const T* grid, T* vis, hipStream_t stream, bool sort_records)
+        const T* grid, T* vis, hipStream_t stream)
 {
     sdp_Error st = SDP_SUCCESS;
     sdp_Error* status = &st;
@@ -2663,16 +2931,12 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         const float* recs = (const float*)s.recs;
         if (p.support <= 16)
         {
-            if (p.support <= 8 && gather_form() == 0)
+            if (p.support <= 8)
             {
                 // Lane-per-entry window gather (no record sort needed).
-#ifndef SDP_WIN_ROWS
-#define SDP_WIN_ROWS 32
-#endif
-#ifndef SDP_WIN_THREADS
-#define SDP_WIN_THREADS 256
-#endif
-                constexpr int kR = SDP_WIN_ROWS, kNT = SDP_WIN_THREADS;
+                // Half-tile windows (40 x 72: twice the workgroups per CU
+                // as the 72 x 72 window, 0.52 -> 0.46 ms at config 2).
+                constexpr int kR = 32, kNT = 256;
                 const uint32_t nb = n_items * (kTile / kR);
                 if (p.do_w)
                     k_gather_win<true, 9, kR, kNT><<<nb, kNT, 0, stream>>>(
@@ -2685,20 +2949,7 @@ int gather(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
                 SDP_HIP_CHECK_LAUNCH(status);
                 return *status;
             }
-            if (p.support <= 8 && sort_records && sort_pieces())
-            {
-                k_sort_pieces<<<n_items, 256, 0, stream>>>(p,
-                        (float*)s.recs, s.bin_start, s.item_start,
-                        s.item_bin);
-                SDP_HIP_CHECK_LAUNCH(status);
-            }
-            if (p.support <= 8 && p.do_w)
-                k_gather_tab<true, 9><<<n_items, 256, 0, stream>>>(p, recs,
-                        s.bin_start, s.item_start, s.item_bin, grid, vis);
-            else if (p.support <= 8)
-                k_gather_tab<false, 9><<<n_items, 256, 0, stream>>>(p, recs,
-                        s.bin_start, s.item_start, s.item_bin, grid, vis);
-            else if (p.do_w)
+            if (p.do_w)
                 k_gather_tab<true, 17><<<n_items, 256, 0, stream>>>(p, recs,
                         s.bin_start, s.item_start, s.item_bin, grid, vis);
             else
@@ -2785,7 +3036,7 @@ int reverse_screen(const ImageParams<T>& ip, int plane, T* dirty,
     template int scatter<T>(const EsParams<T>&, const BucketScratch&, \
             uint32_t, T*, hipStream_t, bool, bool); \
     template int gather<T>(const EsParams<T>&, const BucketScratch&, \
-            uint32_t, const T*, T*, hipStream_t, bool); \
+            uint32_t, const T*, T*, hipStream_t); \
     template int screen_corr_2d<T>(const ImageParams<T>&, const T*, T*, \
             hipStream_t); \
     template int screen_accumulate<T>(const ImageParams<T>&, int, const T*, \

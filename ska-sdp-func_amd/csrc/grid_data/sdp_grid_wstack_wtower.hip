@@ -73,8 +73,25 @@ struct Geo
     int64_t nu, nv, niw, ntask;
     int64_t P0, NP;                  // global w-layer index base and count
     int plane_offset, plane_stride;
+    // Plane set (extension): when plane_mask is set, plane iw is processed
+    // iff mask_first <= iw < mask_first + mask_n and plane_mask[iw -
+    // mask_first] != 0 (offset / stride are then ignored). Device memory.
+    const int* plane_mask;
+    int64_t mask_first, mask_n;
     int fused;                       // sort runs by (group, slot, layer)
 };
+
+// Whether the call processes w-stack plane iw (absolute index).
+__host__ __device__ __forceinline__ bool plane_selected(const Geo& g,
+        int64_t iw)
+{
+    if (g.plane_mask)
+    {
+        const int64_t m = iw - g.mask_first;
+        return m >= 0 && m < g.mask_n && g.plane_mask[m] != 0;
+    }
+    return (iw - g.min_iw) % g.plane_stride == g.plane_offset;
+}
 
 // sdp_gridder_clamp_channels_single / _uv row arithmetic
 // (sdp_gridder_clamp_channels.cpp:37-62).
@@ -161,8 +178,8 @@ __global__ void k_bin(const U* __restrict__ uvw, Geo g, BinOut out)
             &iw_hi);
     for (int64_t iw = iw_lo; iw <= iw_hi; ++iw)
     {
+        if (!plane_selected(g, iw)) continue;
         const int64_t iw_rel = iw - g.min_iw;
-        if (iw_rel % g.plane_stride != g.plane_offset) continue;
         // Visibilities on the w-stack plane (.cpp:336-343 / 612-618).
         const double min_w = iw * g.ws_dist - g.ws_dist / 2;
         const double max_w = (iw + 1) * g.ws_dist - g.ws_dist / 2;
@@ -900,29 +917,13 @@ __host__ __device__ constexpr int prep_stride(int W)
 #ifndef TOWER_IDFT_WAVES
 #define TOWER_IDFT_WAVES 6
 #endif
-// k_tower_dft with 8 waves of one block each (SDP_DFT_NW=8): half the
-// per-lane pixel state, so more waves per SIMD hide the per-layer
-// dependency chains.
-#ifndef TOWER_DFT8_WAVES
-#define TOWER_DFT8_WAVES 6
-#endif
-#ifndef TOWER_IDFT8_WAVES
-#define TOWER_IDFT8_WAVES 8
-#endif
-#ifndef SDP_IDFT_NW
-#define SDP_IDFT_NW 4
-#endif
-#ifndef SDP_DFT_NW
-#define SDP_DFT_NW 4
-#endif
 // k_tower_idft: staged visibilities (ring) and w-layers between re-anchored
-// images (see k_tower_idft).
-#ifndef SDP_IDFT_CAP
-#define SDP_IDFT_CAP 16
-#endif
-#ifndef SDP_IDFT_BLOCK
-#define SDP_IDFT_BLOCK 16
-#endif
+// images (see k_tower_idft). 8-wave workgroups of one block per wave (half
+// the per-lane pixel state, 6-8 waves per SIMD) measured 20.0 -> 22.4 ms
+// (k_tower_dft) and 31.1 -> 35.0 ms (k_tower_idft) per config-4 plane and
+// were removed.
+constexpr int kIdftCap = 16;
+constexpr int kIdftBlock = 16;
 constexpr int kDftCap = 32;      // staged visibilities (ring)
 constexpr int kDftTile = 32;     // tile edge (pixels)
 constexpr int kDftLayers = 512;  // max w-layers of a sub-grid's tower
@@ -955,20 +956,16 @@ struct DftParams
 
 // Tap DFT of a visibility's W kernel taps at one tile row / column:
 // sum_du kt[du] e^{2 pi i (idx + du step) / S} (checkerboard folded into
-// idx and step by the callers). SDP_TOWER_HORNER (default): Horner in
-// z = e^{2 pi i step / S}, then one product with e^{2 pi i idx / S} -- two
-// twiddle-table reads instead of W; the table rows the lanes of a wave read
-// are (a0 + du) l apart, so the W reads per DFT took ~3.5-way LDS bank
-// conflicts on average. f32 rounding of the recurrence: ~W ulp.
-#ifndef SDP_TOWER_HORNER
-#define SDP_TOWER_HORNER 1
-#endif
+// idx and step by the callers): Horner in z = e^{2 pi i step / S}, then one
+// product with e^{2 pi i idx / S} -- two twiddle-table reads instead of W
+// (the per-tap table form: the rows the lanes of a wave read are (a0 + du)
+// l apart, ~3.5-way LDS bank conflicts; 23.3 -> 21.9 ms per plane).
+// f32 rounding of the recurrence: ~W ulp.
 
 __device__ __forceinline__ float2 tap_dft(const float* kt, int W,
         const float2* s_tw, int idx, int step, int S)
 {
 #pragma clang fp contract(off)
-#if SDP_TOWER_HORNER
     const float2 z = s_tw[step], e0 = s_tw[idx];
     float ar = kt[W - 1], ai = 0.0f;
     for (int du = W - 2; du >= 0; --du)
@@ -981,18 +978,6 @@ __device__ __forceinline__ float2 tap_dft(const float* kt, int W,
     }
     return make_float2(__builtin_fmaf(ar, e0.x, -(ai * e0.y)),
             __builtin_fmaf(ar, e0.y, ai * e0.x));
-#else
-    float sr = 0.0f, si = 0.0f;
-    for (int du = 0; du < W; ++du)
-    {
-        const float2 e = s_tw[idx];
-        sr = __builtin_fmaf(kt[du], e.x, sr);
-        si = __builtin_fmaf(kt[du], e.y, si);
-        idx += step;
-        if (idx >= S) idx -= S;
-    }
-    return make_float2(sr, si);
-#endif
 }
 
 // Same, W known at compile time (the common W = 8): the tap reads are
@@ -1020,9 +1005,7 @@ __device__ __forceinline__ float2 tap_dft_w(const float* kt,
 __device__ __forceinline__ float2 tap_dft_any(const float* kt, int W,
         const float2* s_tw, int idx, int step, int S)
 {
-#if SDP_TOWER_HORNER
     if (W == 8) return tap_dft_w<8>(kt, s_tw, idx, step);
-#endif
     return tap_dft(kt, W, s_tw, idx, step, S);
 }
 
@@ -1057,8 +1040,8 @@ __device__ __forceinline__ void stage_records(const DftParams& d, int64_t v0,
 // independent accumulation chains keep the matrix core busier.
 template<typename U, int NB, int NW = 4>
 __global__ __launch_bounds__(64 * NW)
-__attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_DFT8_WAVES :
-        NB == 2 ? TOWER_DFT_WAVES : 1))) void k_tower_dft(
+__attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_DFT_WAVES : 1)))
+void k_tower_dft(
         DftParams d,
         const U* __restrict__ uvws, const Cx<float>* __restrict__ vis)
 {
@@ -1317,8 +1300,8 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_DFT8_WAVES :
 // 32 columns before the one row contraction / partial update per chunk.
 template<typename U, int NB, int NW = 4>
 __global__ __launch_bounds__(64 * NW)
-__attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_IDFT8_WAVES :
-        NB == 2 ? TOWER_IDFT_WAVES : 1))) void k_tower_idft(
+__attribute__((amdgpu_waves_per_eu(NB == 2 ? TOWER_IDFT_WAVES : 1)))
+void k_tower_idft(
         DftParams d, const U* __restrict__ uvws)
 {
 #pragma clang fp contract(off)
@@ -1326,7 +1309,7 @@ __attribute__((amdgpu_waves_per_eu(NW == 8 ? TOWER_IDFT8_WAVES :
     constexpr int NT = 64 * NW, kCW = NW / 2;
     constexpr int kNbOff = 16 * kCW;                 // column step of nb
     constexpr int kCols = kNbOff * NB;               // tile columns
-    constexpr int kCap = SDP_IDFT_CAP, kBlk = SDP_IDFT_BLOCK;
+    constexpr int kCap = kIdftCap, kBlk = kIdftBlock;
     static_assert((kCap & (kCap - 1)) == 0 && kCap >= 16, "ring of >= 16");
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     extern __shared__ float2 s_tw[];                // e^{2 pi i k / S}, S
@@ -1821,17 +1804,11 @@ sdp_fft::Plan2D* cached_plan(int n, bool dbl, size_t batch, size_t dist,
 
 // The w-stack plane FFT (complex float, G a power of two in [1024, 16384]):
 // the fused three-pass FFT (es_fft.hip) in place, output rows permuted,
-// instead of rocFFT's four passes (env SDP_WT_FFT=rocfft keeps rocFFT).
+// instead of rocFFT's four passes (rocFFT for f64 and other sizes).
 const sdp_es::FftTwiddles* plane_fft_twiddles(int64_t G, bool dbl,
         sdp_Error* status)
 {
-    static int use = -1;
-    if (use < 0)
-    {
-        const char* e = getenv("SDP_WT_FFT");
-        use = (e && std::string(e) == "rocfft") ? 0 : 1;
-    }
-    if (!use || dbl || G > INT32_MAX || !sdp_es::fused_fft_supported((int)G))
+    if (dbl || G > INT32_MAX || !sdp_es::fused_fft_supported((int)G))
         return nullptr;
     static std::map<std::pair<int, int64_t>, sdp_es::FftTwiddles> cache;
     const auto key = std::make_pair(current_device(), G);
@@ -2151,16 +2128,6 @@ TowerParams tower_params(const sdp_GridderWtowerUVW* k, const Geo& g,
     return p;
 }
 
-// Fused tower path (k_tower_dft) for complex-float gridding unless
-// SDP_WT_FUSED=0 selects the layer-by-layer path.
-bool dft_enabled()
-{
-    static const bool on = [] {
-        const char* e = std::getenv("SDP_WT_FUSED");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
 
 struct DftData
 {
@@ -2334,7 +2301,7 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
     (void)hipMemGetInfo(&free_b, &total_b);
     const size_t budget = std::max<size_t>(per_slot * 64, free_b / 3);
     Binned b;
-    g.fused = (sizeof(T) == 4 && dft_enabled() && g.S % kDftTile == 0 &&
+    g.fused = (sizeof(T) == 4 && g.S % kDftTile == 0 &&
             g.S <= kDftMaxS && g.w_support <= 16 && g.support <= 16) ? 1 : 0;
     bool any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b, status);
     if (*status) return;
@@ -2428,11 +2395,7 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                 const int tiles = (g.S / kDftTile) *
                         (g.S / (two ? 2 * kDftTile : kDftTile));
                 tower_timing().start();
-                if (two && SDP_DFT_NW == 8)
-                    k_tower_dft<U, 1, 8><<<dim3(tiles, (unsigned)gr.slots),
-                            512, g.S * sizeof(float2)>>>(dp, d_uvw,
-                            (const Cx<float>*)d_vis);
-                else if (two)
+                if (two)
                     k_tower_dft<U, 2><<<dim3(tiles, (unsigned)gr.slots),
                             256, g.S * sizeof(float2)>>>(dp, d_uvw,
                             (const Cx<float>*)d_vis);
@@ -2600,7 +2563,7 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
     (void)hipMemGetInfo(&free_b, &total_b);
     const size_t budget = std::max<size_t>(per_slot * 64, free_b / 3);
     Binned b;
-    g.fused = (sizeof(T) == 4 && dft_enabled() && g.S % kDftTile == 0 &&
+    g.fused = (sizeof(T) == 4 && g.S % kDftTile == 0 &&
             g.S <= kDftMaxS && g.w_support <= 16 && g.support <= 16) ? 1 : 0;
     bool any = bin_visibilities<U>(d_uvw, g, budget, per_slot, &b, status);
     if (*status) return;
@@ -2731,10 +2694,7 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
                 dp.in = (const Cx<float>*)d_wimg;
                 dp.part = d_part;
                 tower_timing().start();
-                if (two && SDP_IDFT_NW == 8)
-                    k_tower_idft<U, 1, 8><<<dim3(ntiles, (unsigned)gr.slots),
-                            512, g.S * sizeof(float2)>>>(dp, d_uvw);
-                else if (two)
+                if (two)
                     k_tower_idft<U, 2><<<dim3(ntiles, (unsigned)gr.slots),
                             256, g.S * sizeof(float2)>>>(dp, d_uvw);
                 else
@@ -2924,24 +2884,48 @@ const U* cptr(const sdp_Mem* m)
     return (const U*)sdp_mem_data_const(m);
 }
 
+// Plane set of the *_plane_set extension: a 1-D int32 mask, host or device
+// (staged), or NULL (offset / stride selection).
+bool check_mask(const sdp_Mem* mask, sdp_Error* status)
+{
+    if (*status || !mask) return !*status;
+    if (sdp_mem_type(mask) != SDP_MEM_INT || sdp_mem_num_dims(mask) != 1 ||
+            !sdp_mem_is_c_contiguous(mask))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("The plane mask must be a 1-D contiguous int32 array");
+        return false;
+    }
+    return true;
+}
+
+void set_mask(Geo& g, const Staged& sm, int64_t first, const sdp_Mem* mask)
+{
+    if (!mask) return;
+    g.plane_mask = (const int*)sdp_mem_data_const(sm.dev);
+    g.mask_first = first;
+    g.mask_n = sdp_mem_shape_dim(mask, 0);
+}
+
 void run_grid(const sdp_Mem* vis, double f0, double df, const sdp_Mem* uvw,
         int S, double theta, double w_step, double hu, double hv,
         int support, int os, int w_support, int wos, double frac, double H,
         int verbosity, sdp_Mem* image, int plane_offset, int plane_stride,
-        sdp_Error* status)
+        int64_t mask_first, const sdp_Mem* mask, sdp_Error* status)
 {
     if (!check_args(vis, uvw, image, S, H, plane_offset, plane_stride,
-            status))
+            status) || !check_mask(mask, status))
         return;
     std::lock_guard<std::mutex> lock(g_mutex);
     const int64_t G = sdp_mem_shape_dim(image, 0);
     sdp_GridderWtowerUVW* k = cached_kernel((int)G, S, theta, w_step, hu, hv,
             support, os, w_support, wos, status);
     if (*status) return;
-    Staged sv, su, si;
+    Staged sv, su, si, sm;
     sv.init(vis, status);
     su.init(uvw, status);
     si.init(image, status);
+    if (mask) sm.init(mask, status);
     if (*status) return;
     // Output image cleared first (.cpp:604-606).
     SDP_HIP_CHECK(hipMemsetAsync(sdp_mem_data(si.dev), 0,
@@ -2949,6 +2933,7 @@ void run_grid(const sdp_Mem* vis, double f0, double df, const sdp_Mem* uvw,
             sdp_mem_type_size(sdp_mem_type(image)), 0), status);
     Geo g = make_geo(vis, f0, df, S, theta, w_step, support, w_support, frac,
             H, plane_offset, plane_stride);
+    set_mask(g, sm, mask_first, mask);
     const AnyView img = {sdp_mem_data(si.dev),
             any_kind(sdp_mem_type(image))};
     const sdp_MemType tv = sdp_mem_type(vis), tu = sdp_mem_type(uvw);
@@ -2972,20 +2957,22 @@ void run_degrid(const sdp_Mem* image, double f0, double df,
         const sdp_Mem* uvw, int S, double theta, double w_step, double hu,
         double hv, int support, int os, int w_support, int wos, double frac,
         double H, int verbosity, sdp_Mem* vis, int plane_offset,
-        int plane_stride, sdp_Error* status)
+        int plane_stride, int64_t mask_first, const sdp_Mem* mask,
+        sdp_Error* status)
 {
     if (!check_args(vis, uvw, image, S, H, plane_offset, plane_stride,
-            status))
+            status) || !check_mask(mask, status))
         return;
     std::lock_guard<std::mutex> lock(g_mutex);
     const int64_t G = sdp_mem_shape_dim(image, 0);
     sdp_GridderWtowerUVW* k = cached_kernel((int)G, S, theta, w_step, hu, hv,
             support, os, w_support, wos, status);
     if (*status) return;
-    Staged sv, su, si;
+    Staged sv, su, si, sm;
     sv.init(vis, status);
     su.init(uvw, status);
     si.init(image, status);
+    if (mask) sm.init(mask, status);
     if (*status) return;
     // Output visibilities cleared first (.cpp:332-334).
     SDP_HIP_CHECK(hipMemsetAsync(sdp_mem_data(sv.dev), 0,
@@ -2993,6 +2980,7 @@ void run_degrid(const sdp_Mem* image, double f0, double df,
             0), status);
     Geo g = make_geo(vis, f0, df, S, theta, w_step, support, w_support, frac,
             H, plane_offset, plane_stride);
+    set_mask(g, sm, mask_first, mask);
     const AnyView img = {sdp_mem_data(si.dev),
             any_kind(sdp_mem_type(image))};
     const sdp_MemType tv = sdp_mem_type(vis), tu = sdp_mem_type(uvw);
@@ -3028,7 +3016,7 @@ void sdp_grid_wstack_wtower_grid_all(const sdp_Mem* vis, double freq0_hz,
     run_grid(vis, freq0_hz, dfreq_hz, uvw, subgrid_size, theta, w_step,
             shear_u, shear_v, support, oversampling, w_support,
             w_oversampling, subgrid_frac, w_tower_height, verbosity, image, 0,
-            1, status);
+            1, 0, nullptr, status);
 }
 
 void sdp_grid_wstack_wtower_degrid_all(const sdp_Mem* image,
@@ -3042,7 +3030,7 @@ void sdp_grid_wstack_wtower_degrid_all(const sdp_Mem* image,
     run_degrid(image, freq0_hz, dfreq_hz, uvw, subgrid_size, theta, w_step,
             shear_u, shear_v, support, oversampling, w_support,
             w_oversampling, subgrid_frac, w_tower_height, verbosity, vis, 0,
-            1, status);
+            1, 0, nullptr, status);
 }
 
 void sdp_grid_wstack_wtower_grid_planes(const sdp_Mem* vis, double freq0_hz,
@@ -3055,7 +3043,27 @@ void sdp_grid_wstack_wtower_grid_planes(const sdp_Mem* vis, double freq0_hz,
     run_grid(vis, freq0_hz, dfreq_hz, uvw, subgrid_size, theta, w_step,
             shear_u, shear_v, support, oversampling, w_support,
             w_oversampling, subgrid_frac, w_tower_height, verbosity, image,
-            plane_offset, plane_stride, status);
+            plane_offset, plane_stride, 0, nullptr, status);
+}
+
+void sdp_grid_wstack_wtower_grid_plane_set(const sdp_Mem* vis,
+        double freq0_hz, double dfreq_hz, const sdp_Mem* uvw,
+        int subgrid_size, double theta, double w_step, double shear_u,
+        double shear_v, int support, int oversampling, int w_support,
+        int w_oversampling, double subgrid_frac, double w_tower_height,
+        int verbosity, sdp_Mem* image, int64_t plane_first,
+        const sdp_Mem* plane_mask, sdp_Error* status)
+{
+    if (!plane_mask && !*status)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("No plane mask given");
+        return;
+    }
+    run_grid(vis, freq0_hz, dfreq_hz, uvw, subgrid_size, theta, w_step,
+            shear_u, shear_v, support, oversampling, w_support,
+            w_oversampling, subgrid_frac, w_tower_height, verbosity, image,
+            0, 1, plane_first, plane_mask, status);
 }
 
 void sdp_grid_wstack_wtower_degrid_planes(const sdp_Mem* image,
@@ -3069,7 +3077,27 @@ void sdp_grid_wstack_wtower_degrid_planes(const sdp_Mem* image,
     run_degrid(image, freq0_hz, dfreq_hz, uvw, subgrid_size, theta, w_step,
             shear_u, shear_v, support, oversampling, w_support,
             w_oversampling, subgrid_frac, w_tower_height, verbosity, vis,
-            plane_offset, plane_stride, status);
+            plane_offset, plane_stride, 0, nullptr, status);
+}
+
+void sdp_grid_wstack_wtower_degrid_plane_set(const sdp_Mem* image,
+        double freq0_hz, double dfreq_hz, const sdp_Mem* uvw,
+        int subgrid_size, double theta, double w_step, double shear_u,
+        double shear_v, int support, int oversampling, int w_support,
+        int w_oversampling, double subgrid_frac, double w_tower_height,
+        int verbosity, sdp_Mem* vis, int64_t plane_first,
+        const sdp_Mem* plane_mask, sdp_Error* status)
+{
+    if (!plane_mask && !*status)
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("No plane mask given");
+        return;
+    }
+    run_degrid(image, freq0_hz, dfreq_hz, uvw, subgrid_size, theta, w_step,
+            shear_u, shear_v, support, oversampling, w_support,
+            w_oversampling, subgrid_frac, w_tower_height, verbosity, vis,
+            0, 1, plane_first, plane_mask, status);
 }
 
 void sdp_grid_wstack_wtower_enable_timing(int enable)

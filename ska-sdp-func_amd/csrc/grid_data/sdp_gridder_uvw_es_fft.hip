@@ -267,6 +267,9 @@ void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
         SDP_HIP_CHECK(hipMalloc(&s.recs1, rec_bytes), status);
         s.recs_bytes = *status ? 0 : rec_bytes;
     }
+    if (!plan->is_double && !plan->do_wstacking && !s.inv_wl)
+        SDP_HIP_CHECK(hipMalloc(&s.inv_wl, sdp_es::kRunMaxChan *
+                sizeof(float)), status);
     const size_t need = sdp_es::bucket_table_entries(
             sdp_es::num_chunks(num_vis, plan->tstride), plan->nbins,
             plan->nsbins);
@@ -603,9 +606,8 @@ void run_degrid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
                 plan->scratch.bin_count, status);
         if (*status) return;
         timing_mark(plan, 3);
-        // The records are sorted for the gather once per bucketing.
         e = sdp_es::gather<T>(es_params<T>(plan, plane), plan->scratch,
-                n_items, grid, vis, plan->stream, plane == 0);
+                n_items, grid, vis, plan->stream);
         if (e) { *status = (sdp_Error)e; return; }
         timing_mark(plan, 4);
         timing_collect_range(plan, 1, 4, kDegridSlots);
@@ -640,6 +642,7 @@ void sdp_gridder_uvw_es_fft_free_plan(sdp_GridderUvwEsFft* plan)
     if (s.bin_count) (void)hipFree(s.bin_count);
     if (s.recs) (void)hipFree(s.recs);
     if (s.recs1) (void)hipFree(s.recs1);
+    if (s.inv_wl) (void)hipFree(s.inv_wl);
     sdp_fft::destroy_2d(plan->fft);
     sdp_es::fft_twiddles_destroy(&plan->fft_tw);
     if (plan->timing)

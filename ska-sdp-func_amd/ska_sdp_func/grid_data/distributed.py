@@ -110,3 +110,83 @@ def predicted_speedup(t_scatter_ms, t_fft_image_ms, world, grid_bytes,
                      "reduce": "measured" if mode in red else
                                f"model ({bus_gbs:.0f} GB/s ring)"}
     return out
+
+
+# W-stack plane sharding for the w-towers imager (config 4): the planes are
+# independent until the image sum (ref sdp_grid_wstack_wtower.cpp:608-713),
+# so each rank grids a SET of planes (sdp_grid_wstack_wtower_grid_plane_set)
+# and the images are reduced once. The sets balance a cost model instead of
+# taking every N-th plane.
+
+C_LIGHT = 299792458.0
+
+
+def wstack_plane_loads(uvw, freq0_hz, dfreq_hz, num_chan, w_step,
+                       w_tower_height):
+    """Visibilities per w-stack plane, as (first_plane, counts).
+
+    Plane iw holds channel c of a row when w (f0 + c df) / c lies in
+    [iw d - d/2, (iw + 1) d - d/2), d = w_tower_height * w_step (the
+    reference's plane cells, sdp_grid_wstack_wtower.cpp:336-343). This is
+    a cost model: the driver's exact channel clamps may move a visibility on
+    a cell boundary to the neighbouring plane, so the range carries one
+    plane of margin on each side. uvw: numpy array or torch tensor (any
+    device)."""
+    import numpy as np
+    d = float(w_tower_height) * float(w_step)
+    try:
+        import torch
+        is_torch = isinstance(uvw, torch.Tensor)
+    except ImportError:
+        is_torch = False
+    if is_torch:
+        w = uvw[:, 2].to(torch.float64)
+    else:
+        w = np.asarray(uvw, dtype=np.float64)[:, 2]
+    planes = []
+    for c in range(int(num_chan)):
+        x = w * ((freq0_hz + c * dfreq_hz) / C_LIGHT)
+        iw = (torch.floor(x / d + 0.5) if is_torch
+              else np.floor(x / d + 0.5))
+        planes.append(iw)
+    if not planes or len(w) == 0:
+        return 0, np.zeros(0, np.int64)
+    if is_torch:
+        allp = torch.cat(planes).to(torch.int64)
+        lo, hi = int(allp.min()), int(allp.max())
+        counts = torch.bincount(allp - lo, minlength=hi - lo + 1).cpu().numpy()
+    else:
+        allp = np.concatenate(planes).astype(np.int64)
+        lo, hi = int(allp.min()), int(allp.max())
+        counts = np.bincount(allp - lo, minlength=hi - lo + 1)
+    counts = np.concatenate([[0], counts, [0]]).astype(np.int64)
+    return lo - 1, counts
+
+
+def assign_planes(loads, world, fixed_cost=0.0):
+    """Plane sets of world ranks balancing sum(load + fixed_cost) over the
+    occupied planes (longest-processing-time greedy: heaviest plane first,
+    each to the least-loaded rank). Empty planes (no modelled load) are
+    dealt round-robin at no cost, so every plane of the range belongs to
+    exactly one rank. Returns (masks[world][n] int32, per-rank costs)."""
+    import numpy as np
+    loads = np.asarray(loads, dtype=np.float64)
+    n = len(loads)
+    masks = np.zeros((world, n), np.int32)
+    cost = np.zeros(world)
+    occupied = [i for i in range(n) if loads[i] > 0]
+    for i in sorted(occupied, key=lambda k: (-loads[k], k)):
+        r = int(np.argmin(cost))
+        masks[r, i] = 1
+        cost[r] += loads[i] + fixed_cost
+    empty = [i for i in range(n) if loads[i] <= 0]
+    for j, i in enumerate(empty):
+        masks[j % world, i] = 1
+    return masks, cost
+
+
+def plane_balance(cost):
+    """max / mean of the per-rank modelled costs (1.0 = perfect)."""
+    import numpy as np
+    cost = np.asarray(cost, dtype=np.float64)
+    return float(cost.max() / cost.mean()) if cost.sum() > 0 else 1.0

@@ -110,6 +110,38 @@ def wstack_wtower_grid_planes(vis, freq0_hz, dfreq_hz, uvw, subgrid_size,
     )
 
 
+def wstack_wtower_grid_plane_set(vis, freq0_hz, dfreq_hz, uvw, subgrid_size,
+                                 theta, w_step, shear_u, shear_v, support,
+                                 oversampling, w_support, w_oversampling,
+                                 subgrid_frac, w_tower_height, verbosity,
+                                 image, plane_first: int, plane_mask):
+    """grid_all restricted to the w-stack planes iw (the reference's plane
+    index) with plane_mask[iw - plane_first] != 0; plane_mask: 1-D int32
+    array (numpy or torch, host or device)."""
+    Lib.sdp_grid_wstack_wtower_grid_plane_set(
+        Mem(vis), freq0_hz, dfreq_hz, Mem(uvw), subgrid_size, theta,
+        w_step, shear_u, shear_v, support, oversampling, w_support,
+        w_oversampling, subgrid_frac, w_tower_height, verbosity, Mem(image),
+        int(plane_first), Mem(plane_mask),
+    )
+
+
+def wstack_wtower_degrid_plane_set(image, freq0_hz, dfreq_hz, uvw,
+                                   subgrid_size, theta, w_step, shear_u,
+                                   shear_v, support, oversampling, w_support,
+                                   w_oversampling, subgrid_frac,
+                                   w_tower_height, verbosity, vis,
+                                   plane_first: int, plane_mask):
+    """degrid_all restricted to the planes of plane_mask (see
+    wstack_wtower_grid_plane_set)."""
+    Lib.sdp_grid_wstack_wtower_degrid_plane_set(
+        Mem(image), freq0_hz, dfreq_hz, Mem(uvw), subgrid_size, theta,
+        w_step, shear_u, shear_v, support, oversampling, w_support,
+        w_oversampling, subgrid_frac, w_tower_height, verbosity, Mem(vis),
+        int(plane_first), Mem(plane_mask),
+    )
+
+
 def wstack_wtower_enable_timing(enable: bool = True):
     """Switch HIP-event timing of the fused tower kernels on (resetting
     the totals) or off."""
@@ -139,6 +171,10 @@ for _name in ("degrid_all", "grid_all"):
 for _name in ("degrid_planes", "grid_planes"):
     Lib.wrap_func(f"sdp_grid_wstack_wtower_{_name}", restype=None,
                   argtypes=[_M] + _COMMON + [_I, _I], check_errcode=True)
+for _name in ("degrid_plane_set", "grid_plane_set"):
+    Lib.wrap_func(f"sdp_grid_wstack_wtower_{_name}", restype=None,
+                  argtypes=[_M] + _COMMON + [ctypes.c_int64, _M],
+                  check_errcode=True)
 Lib.wrap_func("sdp_grid_wstack_wtower_enable_timing", restype=None,
               argtypes=[_I])
 Lib.wrap_func("sdp_grid_wstack_wtower_get_timing", restype=_I,

@@ -210,3 +210,51 @@ def test_predicted_speedup_model():
                           reduce_ms={"grid": 2.0})
     assert m["grid"]["reduce"] == "measured"
     assert abs(m["grid"]["ms"] - (5.0 + 2.0 + 0.4)) < 1e-9
+
+
+def test_assign_planes_balances_config4():
+    """Config 4: 10 M rows with w uniform over exactly 32 w-stack planes of
+    a 34-plane range; 8 ranks balance to within 5 % and every plane of the
+    range belongs to exactly one rank (bench_wtower.py at N > 1)."""
+    from ska_sdp_func.grid_data.distributed import (assign_planes,
+                                                    plane_balance,
+                                                    wstack_plane_loads)
+
+    rng = np.random.default_rng(4)
+    d = 68.0 * 1562.3
+    rows = 400000
+    w = (rng.random(rows) * 32 - 16 - 0.5) * d
+    uvw = np.stack([np.zeros(rows), np.zeros(rows), w], 1)
+    first, loads = wstack_plane_loads(uvw, 299792458.0, 0.0, 1, 1562.3, 68.0)
+    assert loads.sum() == rows
+    assert (loads > 0).sum() == 32
+    for world in (2, 3, 4, 8):
+        masks, cost = assign_planes(loads, world,
+                                    fixed_cost=0.4 * loads.mean())
+        assert np.all(masks.sum(axis=0) == 1)        # a partition
+        assert plane_balance(cost) <= 1.05, (world, cost)
+    # Non-uniform loads (a w distribution peaked at 0): LPT beats % N.
+    w2 = rng.normal(0.0, 4 * d, rows)
+    uvw2 = np.stack([np.zeros(rows), np.zeros(rows), w2], 1)
+    first2, loads2 = wstack_plane_loads(uvw2, 299792458.0, 0.0, 1, 1562.3,
+                                        68.0)
+    masks2, cost2 = assign_planes(loads2, 8)
+    rr = np.array([loads2[r::8].sum() for r in range(8)], dtype=float)
+    assert plane_balance(cost2) <= plane_balance(rr)
+    assert plane_balance(cost2) <= 1.05
+
+
+def test_plane_loads_channels_and_margin():
+    """Multi-channel rows count one visibility per channel on the plane of
+    w f_c / c; the range keeps one empty plane of margin on each side."""
+    from ska_sdp_func.grid_data.distributed import wstack_plane_loads
+
+    d = 1000.0
+    uvw = np.array([[0.0, 0.0, 0.2 * d], [0.0, 0.0, 2.7 * d]])
+    first, loads = wstack_plane_loads(uvw, 299792458.0, 299792458.0 * 0.5, 3,
+                                      d, 1.0)
+    # Row 0: x = 0.2, 0.3, 0.4 d -> plane 0 (x3); row 1: 2.7, 4.05, 5.4 d
+    # -> planes 3, 4, 5.
+    planes = {first + i: int(n) for i, n in enumerate(loads) if n}
+    assert planes == {0: 3, 3: 1, 4: 1, 5: 1}
+    assert loads[0] == 0 and loads[-1] == 0

@@ -168,6 +168,28 @@ def test_grid_all_is_adjoint_and_shards_sum(device):
         vacc += vpart
     _close(acc.cpu().numpy(), gy.cpu().numpy(), 1e-10, border=128)
     _close(vacc.cpu().numpy(), ax.cpu().numpy(), 1e-12)
+    # Load-balanced plane sets (the multi-GPU assignment of
+    # bench_wtower.py): disjoint masks over the modelled plane range, host
+    # and device masks, also sum to the whole.
+    from ska_sdp_func.grid_data.distributed import (assign_planes,
+                                                    wstack_plane_loads)
+    first, loads = wstack_plane_loads(c["uvw"], a[0], a[1], C, c["w_step"],
+                                      c["H"])
+    masks, _ = assign_planes(loads, 3)
+    acc.zero_()
+    vacc.zero_()
+    for k in range(3):
+        m = masks[k] if k != 1 else dev(masks[k])
+        part = torch.zeros_like(gy)
+        g.wstack_wtower_grid_plane_set(dev(y), a[0], a[1], d_uvw, *a[3:], 0,
+                                       part, first, m)
+        acc += part
+        vpart = torch.zeros_like(ax)
+        g.wstack_wtower_degrid_plane_set(dev(x), a[0], a[1], d_uvw, *a[3:],
+                                         0, vpart, first, m)
+        vacc += vpart
+    _close(acc.cpu().numpy(), gy.cpu().numpy(), 1e-10, border=128)
+    _close(vacc.cpu().numpy(), ax.cpu().numpy(), 1e-12)
 
 
 def test_argument_errors(device, case):
