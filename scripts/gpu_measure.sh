@@ -1,17 +1,24 @@
 #!/bin/bash
-# Round-end evidence on one GPU box: the bench.py line (config 2 + config 3
-# + 3-D + CPU baselines), its kernel-trace summary, the PMC traffic passes,
-# the config-4 (w-towers) and config-5 (flagger) lines with their traces.
-#   scripts/gpu_r4_measure.sh OUT [parts: es,traffic,wt,flag]
+# Round-end evidence on one GPU box: the whole GPU suite, the bench.py line
+# (config 2 + config 3 + 3-D + CPU baselines), kernel-trace summaries of
+# config 2 / 3-D and of config 3, the PMC traffic passes, the config-4
+# (w-towers) and config-5 (flagger) lines with their traces.
+#   scripts/gpu_measure.sh OUT [parts: test,es,c3,traffic,wt,flag]
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=${1:-gpurun_out/r4m}
-PARTS=${2:-es,traffic,wt,flag}
+OUT=${1:-gpurun_out/measure}
+PARTS=${2:-test,es,c3,traffic,wt,flag}
 mkdir -p "$OUT"
 stats() {   # kernel_stats.csv of a rocprofv3 output dir -> OUT/NAME
     f=$(find "$1" -name "*kernel_stats.csv" | head -1)
     cp "$f" "$OUT/$2" && find "$1" -name "*.csv" ! -name "*kernel_stats.csv" -delete
 }
+if [[ $PARTS == *test* ]]; then
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 \
+        --timeout-method thread > "$OUT/pytest.log" 2>&1 \
+        || { tail -40 "$OUT/pytest.log"; exit 1; }
+    tail -1 "$OUT/pytest.log"
+fi
 if [[ $PARTS == *es* ]]; then
     timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
         || { tail -20 "$OUT/bench.err"; exit 1; }
@@ -21,6 +28,13 @@ if [[ $PARTS == *es* ]]; then
         --no-cpu-baseline --no-config3 > "$OUT/kt.log" 2>&1 \
         || { tail -5 "$OUT/kt.log"; exit 1; }
     stats "$OUT/kt" bench_kernel_stats.csv || exit 1
+fi
+if [[ $PARTS == *c3* ]]; then
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$OUT/c3kt" -o kt -- python3 bench.py --rows 100000 --steps 1 \
+        --warmup 0 --no-cpu-baseline --no-degrid --no-wstack --c3-steps 2 \
+        > "$OUT/c3kt.log" 2>&1 || { tail -5 "$OUT/c3kt.log"; exit 1; }
+    stats "$OUT/c3kt" c3_kernel_stats.csv || exit 1
 fi
 if [[ $PARTS == *traffic* ]]; then
     scripts/pmc_traffic.sh "$OUT/traffic" --steps 3 --warmup 1 \

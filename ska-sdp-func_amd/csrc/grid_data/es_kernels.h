@@ -36,15 +36,6 @@ constexpr int kGroupChunks = 16;       // chunks per level-2 group (and per
 static_assert(kGroupChunks % kCountChunks == 0, "whole counting workgroups");
 constexpr int kMaxSuperBins = 1024;    // super bins (first bucketing level)
 constexpr int kMaxSuperTiles = 4096;   // tiles per super bin (S^2, S <= 64)
-// Channel runs (2-D f32 gridding with many channels): a row's channels move
-// radially through the uv plane and every tile sees them as one contiguous
-// run, so the records are runs (~4 channels each at config 3) instead of
-// visibilities (es_kernels.hip, "Channel runs").
-constexpr int kRunMinChan = 8;         // channels per row for the run path
-constexpr int kRunMaxChan = 65536;     // run lengths kept in 16 bits
-constexpr int kRunSeg = 8;             // channels per bucketing work unit
-constexpr int kRunWin = 128;           // runs staged per scatter window
-constexpr int kRunMapCap = 1024;       // entries per scatter window (bound)
 constexpr int kTapPolyPairs = 3;       // interior taps 1..6 of W = 8
 constexpr int kTapPolyDeg = 10;        // ~1e-9 relative (f32 Horner ~5e-7)
 
@@ -104,14 +95,6 @@ struct BucketScratch
     size_t recs_bytes = 0;
     size_t table_entries = 0;
     bool gtable_dirty = true;       // group rows not known to be zero
-    // Set by bucket(): the records are channel runs (pieces of <= kPiece
-    // runs), and the tile kernel reads the visibilities, weights and
-    // frequencies of the bucketed call itself.
-    bool runs = false;
-    int run_chan = 0;
-    const void* run_vis = nullptr;
-    const void* run_wt = nullptr;
-    float* inv_wl = nullptr;        // [kRunMaxChan]: per channel freq / c
 };
 
 // Number of visibility chunks used for a given visibility count and count
@@ -136,10 +119,6 @@ bool super_geometry(int ntiles, int* sshift, int* nsuper, int* nsbins);
 // plane p derive the tap (plane_tap) and skip the records off that plane.
 // Record layouts:
 //   grid, 2-D:  {pu, pv, vre*w, vim*w}
-//   grid, 2-D, f32, kRunMinChan <= channels <= kRunMaxChan (channel runs):
-//               {u, v, row * channels + first channel, (length - 1) |
-//               (tile inside its super bin) << 16}, one per (row, tile,
-//               maximal range of consecutive channels touching the tile)
 //   grid, 3-D:  {pu, pv, vre*w, vim*w*flip, pos_w, 0, 0, 0}
 //   degrid:     {pu, pv, flip (2-D) | pos_w*flip (3-D), index bits}
 template<typename T>

@@ -855,9 +855,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(
 // the tile of its first tap (degrid); tile f's records from these chunks
 // occupy [bin_start[f] + table[c0][f], ...), a window of a few hundred
 // bytes per tile that the block fills while it stays in L2.
-// RUNS: channel-run records (one tile each, its index inside the super bin
-// in the high half of word 3).
-template<typename T, int MODE, bool DO_W, bool RUNS = false>
+template<typename T, int MODE, bool DO_W>
 __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
         const uint32_t* __restrict__ stable,
         uint32_t* __restrict__ gtable,
@@ -917,13 +915,6 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
         for (int q = 0; q < kIn; ++q)
         {
             if (e + q * 256 >= e1) break;
-            if constexpr (RUNS)
-            {
-                const int j = (int)(__float_as_uint((float)rec[q][3]) >> 16);
-                const uint32_t pos = atomicAdd(&cur[j], 1u);
-                store_rec<T, kWords>(recs + (size_t)pos * kWords, rec[q]);
-                continue;
-            }
             int u0, u1, v0, v1, tu0, tu1, tv0, tv1;
             tap_range(p, rec[q][0], rec[q][1], u0, u1, v0, v1);
             tile_span<T, MODE>(p, u0, u1, v0, v1, tu0, tu1, tv0, tv1);
@@ -940,255 +931,6 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
     }
 }
 
-
-// Channel runs -------------------------------------------------------------
-//
-// 2-D f32 gridding with kRunMinChan <= C <= kRunMaxChan channels. The
-// channels of a row sit at u * f_c / c * uv_scale, moving radially with f_c,
-// so the channels whose support touches a given tile form contiguous runs
-// (exactly one per (row, tile) for monotonic frequencies; any order of
-// frequencies is handled, a run is a maximal range of consecutive channels).
-// A run is bucketed as ONE 16-byte record {u, v, first visibility index,
-// length - 1 | tile inside its super bin << 16}: ~18 records per row of 64
-// channels at config 3 instead of ~79 visibility records, and the tile
-// kernel reads the visibilities, weights and frequencies itself.
-//
-// Work units: (row, segment of kRunSeg channels). A unit owns the runs that
-// START in its segment and follows each to its end (possibly past the
-// segment), so no run is split. Spans and positions are footprint()'s
-// arithmetic (p.do_w == 0, flip 1).
-struct Span
-{
-    int tu0, tu1, tv0, tv1;     // tile span; empty: tu0 > tu1
-    __device__ bool has(int tu, int tv) const
-    {
-        return tu >= tu0 && tu <= tu1 && tv >= tv0 && tv <= tv1;
-    }
-};
-
-__device__ __forceinline__ Span empty_span()
-{
-    Span s;
-    s.tu0 = 1; s.tu1 = 0; s.tv0 = 1; s.tv1 = 0;
-    return s;
-}
-
-// Tiles touched by a channel of a row (grid mode, 2-D), from the channel's
-// inverse wavelength iwl = freq / c (k_inv_wavelength: the same quotient
-// footprint() forms with flip 1): footprint()'s positions and clamped tap
-// range, then tile_span().
-__device__ __forceinline__ Span chan_span(const EsParams<float>& p, float u,
-        float v, float iwl)
-{
-#pragma clang fp contract(off)
-    const float hs = (float)p.support / 2.0f;
-    const int gmin = -p.G / 2, gmax = (p.G - 1) / 2;
-    const float pu = u * iwl * p.uv_scale, pv = v * iwl * p.uv_scale;
-    const int u0 = max((int)ceilf(pu - hs), gmin);
-    const int u1 = min((int)floorf(pu + hs), gmax);
-    const int v0 = max((int)ceilf(pv - hs), gmin);
-    const int v1 = min((int)floorf(pv + hs), gmax);
-    if (u0 > u1 || v0 > v1) return empty_span();
-    Span s;
-    tile_span<float, MODE_GRID>(p, u0, u1, v0, v1, s.tu0, s.tu1, s.tv0,
-            s.tv1);
-    return s;
-}
-
-// Per channel: freq / c in f32, footprint()'s inverse wavelength (flip 1).
-__global__ void k_inv_wavelength(const float* __restrict__ freq, int n,
-        float* __restrict__ iwl)
-{
-#pragma clang fp contract(off)
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c < n) iwl[c] = (1.0f * freq[c]) / (float)kSpeedOfLight;
-}
-
-__device__ __forceinline__ int super_of(const EsParams<float>& p, int tu,
-        int tv)
-{
-    return (tu >> p.sshift) * p.nsuper + (tv >> p.sshift);
-}
-
-__device__ __forceinline__ uint32_t tile_in_super(const EsParams<float>& p,
-        int tu, int tv)
-{
-    const int m = (1 << p.sshift) - 1;
-    return (uint32_t)(((tu & m) << p.sshift) | (tv & m));
-}
-
-// Run starts of segment [s0, s1): fn(tu, tv) for every (tile, channel) with
-// the tile in the channel's span and not in the previous channel's.
-template<typename F>
-__device__ __forceinline__ void run_starts(const EsParams<float>& p, float u,
-        float v, const float* __restrict__ iwl, int s0, int s1, F&& fn)
-{
-    Span prev = s0 > 0 ? chan_span(p, u, v, iwl[s0 - 1]) : empty_span();
-    for (int c = s0; c < s1; ++c)
-    {
-        const Span cur = chan_span(p, u, v, iwl[c]);
-        for (int tu = cur.tu0; tu <= cur.tu1; ++tu)
-            for (int tv = cur.tv0; tv <= cur.tv1; ++tv)
-                if (!prev.has(tu, tv)) fn(tu, tv);
-        prev = cur;
-    }
-}
-
-// The runs owned by segment [s0, s1) of a row of C channels, each followed
-// to its end: fn(tu, tv, first channel, length). At most 4 runs are open
-// (a support < 64 cells spans at most 2 x 2 tiles).
-template<typename F>
-__device__ __forceinline__ void run_walk(const EsParams<float>& p, float u,
-        float v, const float* __restrict__ iwl, int C, int s0, int s1,
-        F&& fn)
-{
-    Span prev = s0 > 0 ? chan_span(p, u, v, iwl[s0 - 1]) : empty_span();
-    int otu[4], otv[4], ost[4];
-    uint32_t live = 0;
-    for (int c = s0;; ++c)
-    {
-        const Span cur = c < C ? chan_span(p, u, v, iwl[c]) : empty_span();
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-        {
-            if (((live >> k) & 1u) && !cur.has(otu[k], otv[k]))
-            {
-                fn(otu[k], otv[k], ost[k], c - ost[k]);
-                live &= ~(1u << k);
-            }
-        }
-        if (c >= s1)
-        {
-            if (!live) break;
-            continue;
-        }
-        for (int tu = cur.tu0; tu <= cur.tu1; ++tu)
-            for (int tv = cur.tv0; tv <= cur.tv1; ++tv)
-            {
-                if (prev.has(tu, tv)) continue;
-                const int k = __builtin_ctz(~live);   // live has <= 3 bits
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                {
-                    if (q == k)
-                    {
-                        otu[q] = tu;
-                        otv[q] = tv;
-                        ost[q] = c;
-                    }
-                }
-                live |= 1u << k;
-            }
-        prev = cur;
-    }
-}
-
-// Counting pass of the run path: the k_bucket_count tables, counting runs
-// (a run is one record of one tile and its super bin).
-template<int NT>
-__global__ __launch_bounds__(NT) void k_bucket_count_runs(EsParams<float> p,
-        int64_t num_rows, int num_chan, int64_t chunk, int nc,
-        const float* __restrict__ uvw, const float* __restrict__ iwl,
-        uint32_t* __restrict__ stable, uint32_t* __restrict__ gtable)
-{
-    __shared__ uint32_t hist[kBinsPerPass];
-    __shared__ uint32_t shist[kCountChunks][kMaxSuperBins];
-    const int pass_base = blockIdx.y * kBinsPerPass;
-    const int nb = min(kBinsPerPass, p.nbins - pass_base);
-    const bool supers = blockIdx.y == 0;
-    for (int i = threadIdx.x; i < nb; i += NT) hist[i] = 0;
-    if (supers)
-        for (int i = threadIdx.x; i < kCountChunks * kMaxSuperBins; i += NT)
-            (&shist[0][0])[i] = 0;
-    __syncthreads();
-    const int nseg = (num_chan + kRunSeg - 1) / kRunSeg;
-    const int c_first = blockIdx.x * kCountChunks;
-#pragma unroll 1
-    for (int q = 0; q < kCountChunks; ++q)
-    {
-        const int64_t r0 = (int64_t)(c_first + q) * chunk;
-        const int64_t r1 = min(num_rows, r0 + chunk);
-        const uint32_t nunits = r1 > r0 ? (uint32_t)((r1 - r0) * nseg) : 0u;
-        uint32_t* sh = shist[q];
-        for (uint32_t unit = threadIdx.x; unit < nunits; unit += NT)
-        {
-            const uint32_t rl = unit / (uint32_t)nseg;
-            const int s0 = (int)(unit - rl * (uint32_t)nseg) * kRunSeg;
-            const int s1 = min(num_chan, s0 + kRunSeg);
-            const int64_t r = r0 + rl;
-            const float u = uvw[3 * r], v = uvw[3 * r + 1];
-            run_starts(p, u, v, iwl, s0, s1, [&](int tu, int tv) {
-                const int b = fine_bin(p, tu, tv) - pass_base;
-                if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
-                if (supers) atomicAdd(&sh[super_of(p, tu, tv)], 1u);
-            });
-        }
-    }
-    __syncthreads();
-    uint32_t* grow = gtable + (size_t)(c_first / kGroupChunks) * p.nbins +
-            pass_base;
-    for (int i = threadIdx.x; i < nb; i += NT)
-    {
-        const uint32_t n = hist[i];
-        if (n) atomicAdd(&grow[i], n);
-    }
-    if (supers)
-        for (int q = 0; q < kCountChunks && c_first + q < nc; ++q)
-        {
-            uint32_t* row = stable + (size_t)(c_first + q) * p.nsbins;
-            for (int i = threadIdx.x; i < p.nsbins; i += NT)
-                row[i] = shist[q][i];
-        }
-}
-
-// First level of the run path: a chunk's run records by super bin. One
-// thread walks one row's channels once (every row has the same channel
-// count, so the lanes of a wave walk in step) and stores each run at its
-// final position, the chunk's offset in the run's super bin (scanned count
-// table) plus a rank from an LDS atomic. The stores are scattered 16-byte
-// records, but ~4x fewer than visibility records.
-template<int NT>
-__global__ __launch_bounds__(NT) void k_bucket_fill1_runs(EsParams<float> p,
-        int64_t num_rows, int num_chan, int64_t chunk,
-        const float* __restrict__ uvw, const float* __restrict__ iwl,
-        const uint32_t* __restrict__ stable,
-        const uint32_t* __restrict__ bin_count, uint32_t* __restrict__ sb_start,
-        float* __restrict__ recs1)
-{
-    __shared__ uint32_t cursor[kMaxSuperBins];
-    __shared__ uint32_t loff[kMaxSuperBins];
-    __shared__ uint32_t s_wave[NT / 64];
-    const int t = threadIdx.x;
-    const int nsb = p.nsbins;
-    const uint32_t n_sb = block_scan_counts<NT>(bin_count + p.nbins, loff,
-            nsb, s_wave);
-    __syncthreads();
-    const uint32_t* row = stable + (size_t)blockIdx.x * p.nsbins;
-    for (int i = t; i < nsb; i += NT)
-    {
-        cursor[i] = loff[i] + row[i];
-        if (blockIdx.x == 0) sb_start[i] = loff[i];
-    }
-    if (blockIdx.x == 0 && t == 0) sb_start[nsb] = n_sb;
-    __syncthreads();
-    const int64_t r0 = (int64_t)blockIdx.x * chunk;
-    const int64_t r1 = min(num_rows, r0 + chunk);
-    float4* recs4 = (float4*)recs1;
-    for (int64_t r = r0 + t; r < r1; r += NT)
-    {
-        const float u = uvw[3 * r], v = uvw[3 * r + 1];
-        const uint32_t vbase = (uint32_t)(r * num_chan);
-        run_walk(p, u, v, iwl, num_chan, 0, num_chan,
-                [&](int tu, int tv, int c, int n) {
-            const int sb = super_of(p, tu, tv);
-            const uint32_t pos = atomicAdd(&cursor[sb], 1u);
-            recs4[pos] = make_float4(u, v,
-                    __uint_as_float(vbase + (uint32_t)c),
-                    __uint_as_float((uint32_t)(n - 1) |
-                            (tile_in_super(p, tu, tv) << 16)));
-        });
-    }
-}
 
 // Zero the grid cells of tiles that several work items share.
 template<typename T>
@@ -1542,57 +1284,16 @@ __device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
 // 128-255; 256: both axes per thread). The tap tables take 0.29 KB per
 // entry: 128 entries = 40 KB of LDS per workgroup (4 per CU), 96 = 30 KB (5).
 constexpr int kScatterChunk = 128;
-// Inputs of the run path (channel runs, es_kernels.h): the bucketed call's
-// visibilities, weights and frequencies.
-struct RunSrc
-{
-    const float* vis;
-    const float* wt;
-    const float* inv_wl;    // per channel: freq / c, footprint()'s quotient
-    int chan;
-    uint32_t magic;         // floor(2^32 / chan): visibility index -> channel
-};
-
-// Exclusive scan of one value per thread over a 256-thread block; returns
-// the total. s_scan: 4 words of LDS; the caller synchronises before reusing
-// it.
-__device__ __forceinline__ uint32_t block_scan_256(uint32_t x, uint32_t& excl,
-        uint32_t* s_scan)
-{
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t inc = x;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1)
-    {
-        const uint32_t y = __shfl_up(inc, o);
-        if (lane >= o) inc += y;
-    }
-    if (lane == 63) s_scan[wave] = inc;
-    lds_barrier();
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w)
-    {
-        const uint32_t y = s_scan[w];
-        before += w < wave ? y : 0u;
-        total += y;
-    }
-    excl = before + inc - x;
-    return total;
-}
-
-template<bool DO_W, int NTAP, int CHUNK = kScatterChunk, bool RUNS = false>
+template<bool DO_W, int NTAP, int CHUNK = kScatterChunk>
 __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
         const uint32_t* __restrict__ item_bin, float* __restrict__ grid,
-        int flags, RunSrc rs)
+        int flags)
 {
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     static_assert(CHUNK == 256 || (CHUNK <= 128 && CHUNK % 16 == 0),
             "one or two threads per entry");
-    static_assert(!RUNS || (!DO_W && CHUNK <= 128), "runs: 2-D, two threads "
-            "per entry");
     constexpr int kHalf = CHUNK == 256 ? 256 : 128;   // threads per axis
     constexpr int kVec = DO_W ? 2 : 1;
     constexpr int kStride = NTAP + 15;
@@ -1609,14 +1310,6 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     // half and the v half of both are written by the entry's two threads.
     __shared__ uint32_t s_info[CHUNK];
     __shared__ uint32_t s_pos[CHUNK];
-    // Run path: the current window, up to kRunWin runs {u, v, first
-    // visibility index, first entry inside the window | first channel << 11}
-    // and the run of each of its <= kRunMap entries.
-    constexpr int kRunMap = RUNS ? (kRunMapCap / CHUNK) * CHUNK : 1;
-    static_assert(!RUNS || kRunMap < 2048, "11-bit window entry starts");
-    __shared__ float4 s_run[RUNS ? kRunWin : 1];
-    __shared__ uint8_t s_map[kRunMap];
-    __shared__ uint32_t s_scan[4];
 
     const uint32_t item = blockIdx.x;
     if (item_bin[item] == kNoBin) return;
@@ -1657,112 +1350,14 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     }
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rw = r;
-    // Run path: entry e of the window = channel k of run j = s_map[e]; its
-    // inputs are loaded a chunk ahead (raw) and turned into the record
-    // {pu, pv, vre w, vim w} with footprint()'s arithmetic (the per-channel
-    // quotient freq / c from a table) when the chunk is staged.
-    float raw_u = 0.0f, raw_v = 0.0f, raw_iwl = 0.0f, raw_wt = 0.0f;
-    float2 raw_vis = make_float2(0.0f, 0.0f);
-    auto fetch = [&](uint32_t e) {
-        const float4 run = s_run[s_map[e]];
-        const uint32_t w = __float_as_uint(run.w);
-        const uint32_t k = e - (w & 0x7ffu);
-        const uint32_t vi = __float_as_uint(run.z) + k;
-        raw_u = run.x;
-        raw_v = run.y;
-        raw_iwl = rs.inv_wl[(w >> 11) + k];
-        if (stage_v)
-        {
-            raw_vis = *(const float2*)(rs.vis + 2 * (size_t)vi);
-            raw_wt = rs.wt[vi];
-        }
-    };
-    auto raw_rec = [&]() -> float4 {
-#pragma clang fp contract(off)
-        float4 q;
-        q.x = raw_u * raw_iwl * p.uv_scale;
-        q.y = raw_v * raw_iwl * p.uv_scale;
-        q.z = raw_vis.x * raw_wt;
-        q.w = raw_vis.y * raw_wt;
-        return q;
-    };
-    if (!RUNS && et < CHUNK && e0 + et < e1)
+    if (et < CHUNK && e0 + et < e1)
     {
         r = recs4[(size_t)(e0 + et) * kVec];
         if (DO_W) rw = recs4[(size_t)(e0 + et) * kVec + 1];
     }
-    // Run path: windows of <= kRunMap entries (whole chunks) from <=
-    // kRunWin runs, the first possibly entered at an offset (a run longer
-    // than the window's room continues in the next one). One pass over
-    // [e0, e1) otherwise.
-    uint32_t wj = e0, wo = 0;       // window's first run, entry offset in it
-    for (bool more = e0 < e1; more;)
+    for (uint32_t cb = e0; cb < e1; cb += CHUNK)
     {
-    uint32_t c_end = e1, c_begin = e0;
-    more = false;
-    if (RUNS)
-    {
-        // s_run / s_map are free: every read of the previous window
-        // preceded its last B2 barrier.
-        const uint32_t nrun = min((uint32_t)kRunWin, e1 - wj);
-        float4 run = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        uint32_t len = 0;
-        if ((uint32_t)t < nrun)
-        {
-            run = recs4[wj + t];
-            const uint32_t off = t == 0 ? wo : 0u;
-            len = (__float_as_uint(run.w) & 0xffffu) + 1u - off;
-            const uint32_t vi = __float_as_uint(run.z) + off;
-            uint32_t q = __umulhi(vi, rs.magic);
-            if (vi - q * (uint32_t)rs.chan >= (uint32_t)rs.chan) ++q;
-            run.z = __uint_as_float(vi);
-            run.w = __uint_as_float((vi - q * (uint32_t)rs.chan) << 11);
-        }
-        uint32_t excl = 0;
-        const uint32_t tot = block_scan_256(len, excl, s_scan);
-        if ((uint32_t)t < nrun && excl < (uint32_t)kRunMap)
-        {
-            run.w = __uint_as_float(__float_as_uint(run.w) | excl);
-            s_run[t] = run;
-            const uint32_t hi = min(excl + len, (uint32_t)kRunMap);
-            for (uint32_t k = excl; k < hi; ++k) s_map[k] = (uint8_t)t;
-        }
-        lds_barrier();
-        c_begin = 0;
-        c_end = min(tot, (uint32_t)kRunMap);
-        // Next window: after the run holding the window's last entry, or
-        // inside it if it continues past the window.
-        if (tot > (uint32_t)kRunMap)
-        {
-            const uint32_t jl = s_map[kRunMap - 1];
-            const uint32_t ex = __float_as_uint(s_run[jl].w) & 0x7ffu;
-            const uint32_t ln = (jl == 0 ? wo : 0u) +
-                    (uint32_t)kRunMap - ex;   // entries of run jl consumed
-            const uint32_t full = (__float_as_uint(recs4[wj + jl].w) &
-                    0xffffu) + 1u;
-            if (ln < full)
-            {
-                wj += jl;
-                wo = ln;
-            }
-            else
-            {
-                wj += jl + 1;
-                wo = 0;
-            }
-        }
-        else
-        {
-            wj += nrun;
-            wo = 0;
-        }
-        more = wj < e1;
-        if (et < CHUNK && (uint32_t)et < c_end) fetch((uint32_t)et);
-    }
-    for (uint32_t cb = c_begin; cb < c_end; cb += CHUNK)
-    {
-        if (RUNS) r = raw_rec();
-        const int n = (int)min((uint32_t)CHUNK, c_end - cb);
+        const int n = (int)min((uint32_t)CHUNK, e1 - cb);
         // Tap range of this thread's axis (both with CHUNK = 256): same
         // formula as tap_range / footprint.
         const float hs = (float)p.support / 2.0f;
@@ -1851,17 +1446,10 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         }
         // Next chunk's records, issued after this chunk's last use of r so
         // that nothing waits for them before the next staging.
-        if (et < CHUNK && cb + CHUNK + et < c_end)
+        if (et < CHUNK && cb + CHUNK + et < e1)
         {
-            if (RUNS)
-            {
-                fetch(cb + CHUNK + et);
-            }
-            else
-            {
-                r = recs4[(size_t)(cb + CHUNK + et) * kVec];
-                if (DO_W) rw = recs4[(size_t)(cb + CHUNK + et) * kVec + 1];
-            }
+            r = recs4[(size_t)(cb + CHUNK + et) * kVec];
+            if (DO_W) rw = recs4[(size_t)(cb + CHUNK + et) * kVec + 1];
         }
         lds_barrier();   // B2: entry words and tap tables complete
 
@@ -1942,7 +1530,6 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
         }
     }
-    }   // windows
 #pragma unroll
     for (int cblk = 0; cblk < 4; ++cblk)
     {
@@ -2729,13 +2316,6 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
     uint32_t* gtable = s->table;                                   // [ng][nbins]
     uint32_t* stable = s->table + s->table_entries -
             (size_t)nc * p.nsbins;                                 // [nc][nsbins]
-    // Channel runs (2-D f32 gridding with many channels): run records.
-    const bool runs = sizeof(T) == 4 && mode == MODE_GRID && !p.do_w &&
-            num_chan >= kRunMinChan && num_chan <= kRunMaxChan;
-    s->runs = runs;
-    s->run_chan = num_chan;
-    s->run_vis = vis;
-    s->run_wt = weight;
     if (p.nsbins < 1 || p.nsbins > kMaxSuperBins ||
             (1 << (2 * p.sshift)) > kMaxSuperTiles ||
             p.tstride != p.nbins + p.nsbins ||
@@ -2751,26 +2331,7 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
                 sizeof(uint32_t), stream), status);
     if (*status) return *status;
     s->gtable_dirty = true;
-    if constexpr (sizeof(T) == 4)
-    {
-        if (runs)
-        {
-            if (!s->inv_wl)
-            {
-                SDP_LOG_ERROR("Bucketing scratch has no channel table");
-                return SDP_ERR_RUNTIME;
-            }
-            k_inv_wavelength<<<(num_chan + 255) / 256, 256, 0, stream>>>(
-                    freq, num_chan, s->inv_wl);
-            k_bucket_count_runs<1024><<<grid_b, 1024, 0, stream>>>(p,
-                    num_rows, num_chan, chunk, nc, uvw, s->inv_wl, stable,
-                    gtable);
-            SDP_HIP_CHECK_LAUNCH(status);
-        }
-    }
-    if (runs)
-        ;
-    else if (mode == MODE_GRID)
+    if (mode == MODE_GRID)
         launch_count<T, MODE_GRID, 1024>(grid_b, p, num_rows, num_chan,
                 chunk, nc, uvw, freq, stable, gtable, stream);
     else
@@ -2801,22 +2362,7 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
     }
     *n_entries = 0;                  // not known on the host
     *n_items = s->item_capacity;     // upper bound; extra items exit
-    if constexpr (sizeof(T) == 4)
-    {
-        if (runs)
-        {
-            k_bucket_fill1_runs<1024><<<nc, 1024, 0, stream>>>(p, num_rows,
-                    num_chan, chunk, uvw, s->inv_wl, stable, s->bin_count,
-                    s->sb_start, (float*)s->recs1);
-            k_bucket_fill2<float, MODE_GRID, false, true><<<dim3(ng,
-                    p.nsbins), 256, 0, stream>>>(p, nc, stable, gtable,
-                    s->bin_count, s->bin_start, s->sb_start,
-                    (const float*)s->recs1, (float*)s->recs);
-        }
-    }
-    if (runs)
-        ;
-    else if (mode == MODE_GRID)
+    if (mode == MODE_GRID)
     {
         if (p.do_w)
             launch_fill<T, MODE_GRID, true, 1024>(nc, chunk, p, num_rows,
@@ -2857,44 +2403,24 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     {
         const float* recs = (const float*)s.recs;
         const int se = (skip_empty ? 1 : 0) | (accumulate ? 2 : 0);
-        RunSrc rs = {};
-        if (s.runs)
-        {
-            rs.vis = (const float*)s.run_vis;
-            rs.wt = (const float*)s.run_wt;
-            rs.inv_wl = s.inv_wl;
-            rs.chan = s.run_chan;
-            rs.magic = (uint32_t)(0x100000000ull / (uint64_t)s.run_chan);
-        }
         if (p.support <= 16)
         {
-#ifndef SDP_RUNS_CHUNK
-#define SDP_RUNS_CHUNK 112
-#endif
-            if (s.runs && p.support <= 8)
-                k_scatter_tab<false, 9, SDP_RUNS_CHUNK, true><<<n_items, 256, 0,
-                        stream>>>(p, recs, s.bin_start, s.item_start,
-                        s.item_bin, grid, se, rs);
-            else if (s.runs)
-                k_scatter_tab<false, 17, 128, true><<<n_items, 256, 0,
-                        stream>>>(p, recs, s.bin_start, s.item_start,
-                        s.item_bin, grid, se, rs);
-            else if (p.support <= 8 && p.do_w)
+            if (p.support <= 8 && p.do_w)
                 k_scatter_tab<true, 9><<<n_items, 256, 0, stream>>>(
                         p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                        se, rs);
+                        se);
             else if (p.support <= 8)
                 k_scatter_tab<false, 9><<<n_items, 256, 0, stream>>>(
                         p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                        se, rs);
+                        se);
             else if (p.do_w)
                 k_scatter_tab<true, 17><<<n_items, 256, 0, stream>>>(
                         p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                        se, rs);
+                        se);
             else
                 k_scatter_tab<false, 17><<<n_items, 256, 0, stream>>>(
                         p, recs, s.bin_start, s.item_start, s.item_bin, grid,
-                        se, rs);
+                        se);
             SDP_HIP_CHECK_LAUNCH(status);
             return *status;
         }

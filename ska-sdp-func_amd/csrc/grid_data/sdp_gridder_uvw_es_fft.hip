@@ -267,9 +267,6 @@ void ensure_scratch(sdp_GridderUvwEsFft* plan, int64_t num_vis,
         SDP_HIP_CHECK(hipMalloc(&s.recs1, rec_bytes), status);
         s.recs_bytes = *status ? 0 : rec_bytes;
     }
-    if (!plan->is_double && !plan->do_wstacking && !s.inv_wl)
-        SDP_HIP_CHECK(hipMalloc(&s.inv_wl, sdp_es::kRunMaxChan *
-                sizeof(float)), status);
     const size_t need = sdp_es::bucket_table_entries(
             sdp_es::num_chunks(num_vis, plan->tstride), plan->nbins,
             plan->nsbins);
@@ -642,7 +639,6 @@ void sdp_gridder_uvw_es_fft_free_plan(sdp_GridderUvwEsFft* plan)
     if (s.bin_count) (void)hipFree(s.bin_count);
     if (s.recs) (void)hipFree(s.recs);
     if (s.recs1) (void)hipFree(s.recs1);
-    if (s.inv_wl) (void)hipFree(s.inv_wl);
     sdp_fft::destroy_2d(plan->fft);
     sdp_es::fft_twiddles_destroy(&plan->fft_tw);
     if (plan->timing)

@@ -177,26 +177,6 @@ __device__ __forceinline__ void set_flag(int32_t* row, int j, int P, int lane)
     *(int32_t*)(base + (uint32_t)(lane * P) * 4u) = 1;
 }
 
-// The same without a branch: a raw buffer store over the row whose offset
-// lies past the buffer's range for an unset flag (the hardware drops it), so
-// no exec-mask save / restore per element. rows: the time step's flag row.
-struct FlagRow
-{
-    __amdgpu_buffer_rsrc_t rs;
-    __device__ FlagRow(int32_t* row, int C, int P)
-    {
-        rs = __builtin_amdgcn_make_buffer_rsrc(row, 0,
-                (int)((uint32_t)C * (uint32_t)P * 4u), 0x00020000);
-    }
-    __device__ __forceinline__ void set_if(bool f, int j, int P,
-            int lane) const
-    {
-        const uint32_t off = f ? (uint32_t)((lane + 64 * j) * P) * 4u :
-                0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b32(1, rs, off, 0, 0);
-    }
-};
-
 
 // Key sets: key(j), j < N, from a register array or computed on the fly
 // (a statistic's keys are then never held as an array: they are rebuilt in
@@ -490,19 +470,6 @@ __device__ __forceinline__ ZTest make_ztest(double med, double dev,
     return z;
 }
 
-// z_exceeds by the reciprocal only; near: the value lies within the band
-// where only the exact division decides (the caller re-tests those lanes
-// with z_exceeds). Valid when zt.fast and !zt.dev0.
-__device__ __forceinline__ bool z_exceeds_fast(const ZTest& zt, double val,
-        bool& near)
-{
-#pragma clang fp contract(off)
-    const double num = 0.6795 * (val - zt.med);
-    const double aq = fabs(num * zt.inv);
-    near = fabs(aq - zt.thr) <= zt.band;    // false for NaN, as z_exceeds
-    return aq > zt.thr;
-}
-
 __device__ __forceinline__ bool z_exceeds(const ZTest& zt, double val)
 {
 #pragma clang fp contract(off)
@@ -708,47 +675,18 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
             situation = zmed > prm.thr_bb || zmed < -prm.thr_bb;
         }
 
-        // Magnitude triggers (:214-241) into trig_all. The z-tests run by
-        // the reciprocal for every element (bit j of tbits); the elements
-        // within the band of the threshold take the exact division after
-        // the loop, if any lane has one (rare): no per-element branch.
+        // Magnitude triggers (:214-241) into trig_all.
         {
             const ZTest zt = make_ztest(median, mediandev, prm.thr_mag);
-            uint32_t tbits = 0, nbits = 0;
-            if (zt.fast && !zt.dev0)
-            {
-#pragma unroll
-                for (int j = 0; j < EPL; ++j)
-                {
-                    bool nr;
-                    const bool tr = z_exceeds_fast(zt, (double)m[j], nr);
-                    tbits |= (uint32_t)tr << j;
-                    nbits |= (uint32_t)nr << j;
-                }
-            }
-            else
-            {
-                nbits = (EPL == 32) ? ~0u : ((1u << EPL) - 1u);
-            }
-            if (__builtin_amdgcn_ballot_w64(nbits != 0))
-            {
-#pragma unroll
-                for (int j = 0; j < EPL; ++j)
-                    if ((nbits >> j) & 1u)
-                    {
-                        const bool tr = z_exceeds(zt, (double)m[j]);
-                        tbits = (tbits & ~(1u << j)) | ((uint32_t)tr << j);
-                    }
-            }
-            const FlagRow fr(frow, C, P);
 #pragma unroll
             for (int j = 0; j < EPL; ++j)
             {
                 const bool tr = ch_ok[j] &&
-                        (situation || ((tbits >> j) & 1u));
+                        (situation || z_exceeds(zt, (double)m[j]));
                 const int c = lane + 64 * j;
                 if (prm.window > 0 && ch_ok[j]) trig_all[c] = tr ? 1 : 0;
-                if (prm.window == 0) fr.set_if(tr, j, P, lane);
+                if (prm.window == 0 && tr)
+                    set_flag(frow, j, P, lane);
             }
         }
 
@@ -776,37 +714,10 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
                         k_s, prm.ns, tk_vdev, (uint64_t*)cand, lane, 5);
             }
             const ZTest zv = make_ztest(medianvar, mediandevvar, prm.thr_var);
-            uint32_t vbits = 0, nbits = 0;
-            if (zv.fast && !zv.dev0)
-            {
-#pragma unroll
-                for (int j = 0; j < EPL; ++j)
-                {
-                    bool nr;
-                    const bool tv = z_exceeds_fast(zv, fabs(transit[j]), nr);
-                    vbits |= (uint32_t)tv << j;
-                    nbits |= (uint32_t)nr << j;
-                }
-            }
-            else
-            {
-                nbits = (EPL == 32) ? ~0u : ((1u << EPL) - 1u);
-            }
-            if (__builtin_amdgcn_ballot_w64(nbits != 0))
-            {
-#pragma unroll
-                for (int j = 0; j < EPL; ++j)
-                    if ((nbits >> j) & 1u)
-                    {
-                        const bool tv = z_exceeds(zv, fabs(transit[j]));
-                        vbits = (vbits & ~(1u << j)) | ((uint32_t)tv << j);
-                    }
-            }
-            const FlagRow fr(frow, C, P), fp(fprev, C, P);
 #pragma unroll
             for (int j = 0; j < EPL; ++j)
             {
-                const bool tv = ch_ok[j] && ((vbits >> j) & 1u);
+                const bool tv = ch_ok[j] && z_exceeds(zv, fabs(transit[j]));
                 const int c = lane + 64 * j;
                 if (prm.window > 0)
                 {
@@ -816,10 +727,10 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
                         if (tv) trig_all[c] = 1;
                     }
                 }
-                else
+                else if (tv)
                 {
-                    fr.set_if(tv, j, P, lane);
-                    fp.set_if(tv, j, P, lane);
+                    set_flag(frow, j, P, lane);
+                    set_flag(fprev, j, P, lane);
                 }
             }
         }

@@ -1,16 +1,14 @@
-"""GPU parity of the channel-run path of the ES gridder (2-D, f32, 8 to 65536
-channels per row; es_kernels.hip "Channel runs").
-
-With many channels a row's visibilities are bucketed as runs of consecutive
-channels per grid tile and the tile kernel reads the visibilities, weights
-and frequencies itself. These cases push the run bookkeeping: channel counts
-that are not a multiple of the work-unit segment, descending and shuffled
-frequencies (runs of one tile split), channels whose taps leave the grid,
+"""GPU parity of multi-channel 2-D gridding (f32, 8 to 64 channels per row)
+at the edges of the bucketing: channel counts that are not a multiple of
+anything convenient, descending and shuffled frequencies (the channels of
+a row then jump between tiles), channels whose taps leave the grid,
 exact-integer positions (W + 1 taps), W = 16 and W = 4 plans, tiles with
-more runs than one work item (pieces combined by atomics) and more than one
-run window, the split scatter API and row batches. Reference: the oracle
-(oracle/es_oracle.c, a restatement of sdp_gridder_uvw_es_fft_kernels.cu:
-277-422), relative L2 <= 1e-5 (f32, BASELINE north star).
+more entries than one work item (pieces combined by atomics), the split
+scatter API and row batches. (Written for the round-5 channel-run
+bucketing, which was measured and removed)
+Reference: the oracle (oracle/es_oracle.c, a restatement of
+sdp_gridder_uvw_es_fft_kernels.cu:277-422), relative L2 <= 1e-5 (f32,
+BASELINE north star).
 """
 import numpy as np
 import pytest
@@ -50,23 +48,23 @@ def _grid(device, uvw, freq, vis, wt, n, px, eps, cap=None):
 
 
 @pytest.mark.parametrize("rows,chan,n,eps,frac,order", [
-    (20000, 8, 256, 1e-5, 0.45, "ascending"),    # kRunMinChan
-    (5000, 13, 256, 1e-5, 0.45, "descending"),   # 13 = 8 + 5 (segments)
+    (20000, 8, 256, 1e-5, 0.45, "ascending"),
+    (5000, 13, 256, 1e-5, 0.45, "descending"),
     (3000, 24, 256, 1e-5, 0.45, "shuffled"),     # non-monotonic channels
     (3000, 16, 128, 1e-5, 0.7, "ascending"),     # channels leave the grid
     (3000, 16, 256, 1e-7, 0.45, "ascending"),    # W = 16, 17-slot tables
     (40000, 64, 840, 0.05, 0.45, "ascending"),   # W = 4, G = 1024
 ])
-def test_runs_grid_matches_oracle(device, rows, chan, n, eps, frac, order):
+def test_multichan_grid_matches_oracle(device, rows, chan, n, eps, frac, order):
     uvw, freq, vis, wt, px = make_case(21, rows, chan, n, frac=frac)
     freq = _order(freq, order, 22)
     out, ref = _grid(device, uvw, freq, vis, wt, n, px, eps)
     assert rel_l2(out, ref) < 1e-5
 
 
-def test_runs_integer_positions(device):
+def test_multichan_integer_positions(device):
     """u = v = 0 rows: every channel at an exact integer position (W + 1
-    taps), all channels in one tile: one run of the whole row."""
+    taps), all channels of the row in one tile."""
     n = 128
     uvw, freq, vis, wt, px = make_case(23, 800, 10, n, frac=0.7)
     uvw[:40, :2] = 0.0
@@ -74,25 +72,24 @@ def test_runs_integer_positions(device):
     assert rel_l2(out, ref) < 1e-5
 
 
-def test_runs_hot_tile_pieces_and_windows(device):
-    """All rows in the central tiles: > kPiece (4096) runs in a tile (several
-    work items, combined by atomics into a zeroed tile) and > kRunWin (256)
-    runs per work item (several run windows)."""
+def test_multichan_hot_tile_pieces(device):
+    """All rows in the central tiles: > kPiece (4096) entries in a tile
+    (several work items, combined by atomics into a zeroed tile)."""
     n = 256
     uvw, freq, vis, wt, px = make_case(24, 12000, 8, n, frac=0.01)
     out, ref = _grid(device, uvw, freq, vis, wt, n, px, 1e-5)
     assert rel_l2(out, ref) < 1e-5
 
 
-def test_runs_batched(device):
-    """Row batches of the run path add their tiles to one grid."""
+def test_multichan_batched(device):
+    """Row batches of a multi-channel call add their tiles to one grid."""
     n = 256
     uvw, freq, vis, wt, px = make_case(25, 9000, 16, n)
     out, ref = _grid(device, uvw, freq, vis, wt, n, px, 1e-5, cap=40000)
     assert rel_l2(out, ref) < 1e-5
 
 
-def test_runs_scatter_grid_cells(device):
+def test_multichan_scatter_grid_cells(device):
     """The uv grid of the split API (sdp_grid_uvw_es_fft_scatter) cell by
     cell against the oracle's scatter."""
     import torch
