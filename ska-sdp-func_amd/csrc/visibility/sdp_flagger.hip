@@ -9,10 +9,11 @@
 // patterns (all the values ranked are >= 0, so bit-pattern order is value
 // order). Each statistic is bracketed by its value at the previous time
 // step: one counting pass (compare + ballot + popcount per register) checks
-// that the bracket holds the k-th key and compacts the ~100 keys inside it
-// into LDS, and a bitwise search over those few registers finishes it --
-// no sort. A bracket miss falls back to the search over all keys, so the
-// result never depends on the bracket. The stream state (previous
+// that the bracket holds the k-th key and compacts the ~64 keys inside it
+// into LDS, and radix rounds over those two registers (an LDS histogram of
+// 64 digit ranges and a cross-lane scan per round) finish it -- no sort. A
+// bracket miss falls back to a bitwise search over all keys, so the result
+// never depends on the bracket. The stream state (previous
 // magnitudes, transit scores) stays in registers across time steps; the
 // median history is a per-wave LDS ring; window flagging reads trigger
 // bytes from LDS. Flags are written only where set (idempotent stores of
@@ -46,6 +47,7 @@ struct FlagParams
 // cabsf(z) = hypotf, computed in double and rounded once to float;
 // cabs(z) = glibc's hypot (its non-FMA kernel, sysdeps/ieee754/dbl-64
 // e_hypot.c of glibc 2.35). Both reproduced operation for operation.
+
 __device__ __forceinline__ double mag_of(float re, float im)
 {
 #pragma clang fp contract(off)
@@ -123,7 +125,7 @@ __device__ __forceinline__ int mid_index(int n)
 // select_tracked() brackets each statistic by the previous time step's value
 // (x +- w per statistic and stream): one pass counts the keys below and inside
 // the bracket and compacts the inside ones into LDS; if the k-th key is inside
-// and the bracket holds <= 64 R keys, the search runs on R registers of
+// and the bracket holds <= 64 R keys, radix_select() runs on R registers of
 // candidates instead of all of them. A miss falls back to the search over all
 // keys (still exact); w adapts so that the bracket holds ~32 R candidates.
 // Results never depend on the bracket -- only the cost does.
@@ -242,6 +244,78 @@ __device__ __forceinline__ K search(const Keys& key, int k, K prefix,
     {
         const K kj = key(j);
         const uint64_t m = ballot(kj >= L) & ballot(kj < U);
+        if (m) ans = readlane(kj, (int)__builtin_ctzll(m));
+    }
+    return ans;
+}
+
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Inclusive prefix sum over the 64 lanes: DPP row shifts inside rows of
+// 16, then the row broadcasts (no LDS round trips).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+    return x;
+}
+
+// Radix rounds for the k-th smallest of the n keys inside [L, U) (keys
+// outside it do not take part). A round splits [L, U) into 64 digit
+// ranges of 2^shift keys, counts the keys of each in an LDS histogram
+// (one ds_add per register), scans the 64 counts across the lanes and
+// keeps the digit range that holds the k-th key: ~6 key bits per round,
+// ~30 instructions, against one compare + ballot + popcount probe per bit
+// of the bitwise search. Ends when the range holds a single key (read out)
+// or a single value (ties). bins: 64 words of LDS.
+template<typename K, int N, class Keys>
+__device__ __forceinline__ K radix_select(const Keys& key, int k, K L, K U,
+        int n, uint32_t* bins, int lane, int& nround)
+{
+    while (n > 1 && U - L > 1)
+    {
+        const K span = U - L;
+        const int len = (int)(8 * sizeof(K)) - (sizeof(K) == 8 ?
+                __clzll((long long)(span - 1)) : __clz((int)(span - 1)));
+        const int shift = len > 6 ? len - 6 : 0;
+        bins[lane] = 0u;
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+        {
+            const K d = key(j) - L;
+            if (d < span)
+                __hip_atomic_fetch_add(&bins[(uint32_t)(d >> shift)], 1u,
+                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+        wave_sync();
+        const uint32_t cnt = bins[lane];
+        const uint32_t incl = wave_incl_scan(cnt);
+        const uint64_t over = __builtin_amdgcn_ballot_w64(incl > (uint32_t)k);
+        const int b = (int)__builtin_ctzll(over);
+        k -= (int)__builtin_amdgcn_readlane((int)(incl - cnt), b);
+        n = __builtin_amdgcn_readlane((int)cnt, b);
+        L += (K)b << shift;
+        const K top = L + ((K)1 << shift);
+        if (top < U) U = top;
+        ++nround;
+        wave_sync();
+    }
+    if (n > 1 || U - L <= 1) return L;      // one value left (ties)
+    K ans = L;                              // the one key in [L, U)
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+    {
+        const K kj = key(j);
+        const uint64_t m = ballot(kj - L < U - L);
         if (m) ans = readlane(kj, (int)__builtin_ctzll(m));
     }
     return ans;
@@ -367,22 +441,31 @@ __device__ __forceinline__ V select_tracked(const Keys& key, int k,
     }
     int nprobe = 0;
     K ans;
-    if (kCompact && use_cand)
+    if (hit && (use_cand || !kCompact))
     {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        K c[kCompact ? R : 1];
-#pragma unroll
-        for (int r = 0; r < (kCompact ? R : 1); ++r)
+        // The bracket holds the k-th key: radix rounds over the compacted
+        // candidates (or, N <= R, over the keys themselves).
+        uint32_t* bins = (uint32_t*)(cand_lds + kCap + 2);
+        if (kCompact)
         {
-            const int s = lane + 64 * r;
-            c[r] = s < n_in ? cand_lds[s] : ~(K)0;
+            wave_sync();
+            K c[kCompact ? R : 1];
+#pragma unroll
+            for (int r = 0; r < (kCompact ? R : 1); ++r)
+            {
+                const int s = lane + 64 * r;
+                c[r] = s < n_in ? cand_lds[s] : ~(K)0;
+            }
+            ans = radix_select<K, kCompact ? R : 1>(
+                    ArrayKeys<K, kCompact ? R : 1>{c}, kk, L, U, n_in, bins,
+                    lane, nprobe);
         }
-        ans = search<K, kCompact ? R : 1, false>(
-                ArrayKeys<K, kCompact ? R : 1>{c}, kk, prefix, bit, L, U, c0,
-                c1, nprobe);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        else
+        {
+            ans = radix_select<K, N>(key, kk - c0, L, U, c1 - c0, bins,
+                    lane, nprobe);
+        }
+        wave_sync();
     }
     else
     {
@@ -403,22 +486,26 @@ __device__ __forceinline__ V select_tracked(const Keys& key, int k,
     }
 #endif
     const double a = (double)val_of(ans);
-    const double target = fmin(32.0 * R, fmax(1.0, 0.125 * nvalid));
+    // The width factor only steers the cost: single precision with the
+    // hardware reciprocal (a double division here was ~12 instructions per
+    // selection, 6 selections per step).
+    const float target = fminf(32.0f * R, fmaxf(1.0f, 0.125f * nvalid));
+    const float inv_in = __builtin_amdgcn_rcpf((float)(n_in > 1 ? n_in : 1));
     if (!tr.valid)
     {
         tr.w = a * 0x1p-7;
     }
     else if (hit && attempt == 0)
     {
-        double f = target / (n_in > 1 ? n_in : 1);
-        if (n_in <= kCap) f = f < 0.5 ? 0.5 : (f > 2.0 ? 2.0 : f);
-        tr.w *= f;
+        float f = target * inv_in;
+        if (n_in <= kCap) f = f < 0.5f ? 0.5f : (f > 2.0f ? 2.0f : f);
+        tr.w *= (double)f;
     }
     else if (hit)
     {
         // Found one step beyond the bracket (a 4 w wide window): widen.
-        double f = 2.0 * target / (n_in > 1 ? n_in : 1);
-        tr.w *= f < 1.0 ? 1.0 : (f > 2.0 ? 2.0 : f);
+        const float f = 2.0f * target * inv_in;
+        tr.w *= (double)(f < 1.0f ? 1.0f : (f > 2.0f ? 2.0f : f));
     }
     else if (!(tr.w > 0.0))
     {
@@ -488,12 +575,6 @@ __device__ __forceinline__ bool z_exceeds(const ZTest& zt, double val)
     return z > zt.thr || z < -zt.thr;
 }
 
-__device__ __forceinline__ void wave_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
 // Window spread (:224-240, :316-337): channel d is flagged if it triggered,
 // or a trigger sits i <= window channels above it and d > 0, or i <= window
 // channels below it.
@@ -509,24 +590,20 @@ __device__ __forceinline__ bool spread(const uint8_t* trig, int d, int C,
     return f;
 }
 
-// Occupancy targets (tuning hook: -DFLAGGER_WAVES=...): the float kernels fit 128 VGPRs (4 waves per SIMD) with
-// a few dwords of spill, which measures faster than 3 waves without; the
-// double kernels (two registers per statistic key) stay at 3.
-#ifndef FLAGGER_WAVES
+// Occupancy: the float kernels fit 128 VGPRs (4 waves per SIMD) with a few
+// dwords of spill, which measures faster than 3 waves without; the double
+// kernels (two registers per statistic key) stay at 3. Two candidate
+// registers (128 keys) measured faster than one, three or four.
 #define FLAGGER_WAVES \
     __attribute__((amdgpu_waves_per_eu(sizeof(FP) == 4 ? 4 : 3)))
-#endif
-#ifndef FLAGGER_CAND_REGS
-#define FLAGGER_CAND_REGS 2
-#endif
-constexpr int kCandRegs = FLAGGER_CAND_REGS;   // compacted candidates: 64 per register
+constexpr int kCandRegs = 2;   // compacted candidates: 64 per register
 
 // Per-wave LDS layout: median history | trigger bytes (all, variation) |
-// candidate keys.
+// candidate keys | radix-round histogram.
 __host__ __device__ inline size_t lds_per_wave(int wmh, int C)
 {
     return (size_t)wmh * 8 + 2 * (size_t)((C + 15) & ~15) +
-            (64 * kCandRegs + 2) * 8;
+            (64 * kCandRegs + 2) * 8 + 68 * 4;
 }
 
 // FULL: sampling_step 1 and C == 64 EPL, so every register slot is a sampled
@@ -774,10 +851,8 @@ sdp_Error launch_epl(const FP* vis, int32_t* flags, const FlagParams& prm)
     };
     if (prm.wmh <= 64)
         run(k_flagger<FP, EPL, 1, FULL>);
-#ifndef SDP_FLAGGER_DEV
     else
         run(k_flagger<FP, EPL, 16, FULL>);
-#endif
     SDP_HIP_CHECK_LAUNCH(&st);
     return st;
 }
@@ -793,10 +868,6 @@ sdp_Error launch_full(const FP* vis, int32_t* flags, const FlagParams& prm)
 template<typename FP>
 sdp_Error launch(const FP* vis, int32_t* flags, const FlagParams& prm)
 {
-#ifdef SDP_FLAGGER_DEV   // register-pressure experiments: one kernel only
-    if (sizeof(FP) == 4) return launch_epl<FP, 16, true>(vis, flags, prm);
-    return SDP_ERR_RUNTIME;
-#else
     const int epl = (prm.C + 63) / 64;
     if (epl <= 1) return launch_full<FP, 1>(vis, flags, prm);
     if (epl <= 2) return launch_full<FP, 2>(vis, flags, prm);
@@ -804,7 +875,6 @@ sdp_Error launch(const FP* vis, int32_t* flags, const FlagParams& prm)
     if (epl <= 8) return launch_full<FP, 8>(vis, flags, prm);
     if (epl <= 16) return launch_full<FP, 16>(vis, flags, prm);
     return launch_full<FP, 32>(vis, flags, prm);
-#endif
 }
 
 // Argument checks of the reference (check_params_dynamic,
