@@ -1268,21 +1268,24 @@ __device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
 // ku (x) (kv w V), applied four visibilities per v_mfma_f32_16x16x4_f32.
 // The ES taps are evaluated ONCE per bucketed entry, in chunks of CHUNK =
 // 128 entries: thread t < 128 evaluates entry t's NTAP u-taps, thread
-// t + 128 its v-taps times the weighted visibility (checkerboard signs
-// folded in), each with its own axis's tap range, band mask and table
-// position. The tables are zero-padded: entry e's taps sit at kLead +
-// e * kStride in rows of NTAP + 15 slots whose tail (and the lead before
-// entry 0) stays zero, so the 16 rows (columns) of a sub-tile read taps
-// d0 + i, d0 in [-15, NTAP), with no range check. A visit is one word
-// {u index of row 0, v index of column 0}: the entry's word plus a
-// per-(band, column block) constant, written by ballot compaction into
-// the wave's list of each column block, and the matrix loop spends two
-// vector operations per operand. Barriers are LDS-only and the next
-// chunk's records load after this chunk's staging (no s_waitcnt vmcnt
-// before the visit loops).
+// t + 128 its v-taps and stores the weighted visibility (checkerboard sign
+// folded in) once per entry, each with its own axis's tap range, band mask
+// and table position. The tables are zero-padded: entry e's taps sit at
+// kLead + e * kStride in rows of NTAP + 15 slots whose tail (and the lead
+// before entry 0) stays zero, so the 16 rows (columns) of a sub-tile read
+// taps d0 + i, d0 in [-15, NTAP), with no range check. A visit is {u index
+// of row 0, v index of column 0} (the entry's word plus a per-(band,
+// column block) constant) and the entry number, written by ballot
+// compaction into the wave's list of each column block; the matrix loop
+// forms the B operand as v-tap x visibility (the visibility read is a
+// broadcast). Barriers are LDS-only and the next chunk's records load
+// after this chunk's staging (no s_waitcnt vmcnt before the visit loops).
 // Entries per chunk (<= 128: u taps staged by threads 0-127, v taps by
-// 128-255; 256: both axes per thread). The tap tables take 0.29 KB per
-// entry: 128 entries = 40 KB of LDS per workgroup (4 per CU), 96 = 30 KB (5).
+// 128-255; 256: both axes per thread). Real v-tap rows + one visibility
+// per entry (round 5; the rows held v-tap x visibility as float2 before)
+// take 31 KB of LDS per workgroup at W <= 8: 5 workgroups per CU instead
+// of 4 (tile kernel 0.461 -> 0.447 ms at config 2, 26.1 -> 25.3 ms at
+// config 3, 4.42 -> 4.24 ms for 10 w-planes).
 constexpr int kScatterChunk = 128;
 template<bool DO_W, int NTAP, int CHUNK = kScatterChunk>
 __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
@@ -1302,8 +1305,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     static_assert(kTab < 65536, "16-bit table indices");
     static_assert(kLead % 4 == 0 && kStride % 4 == 0, "16-byte table rows");
     __shared__ __attribute__((aligned(16))) float s_ku[kTab];
-    __shared__ __attribute__((aligned(16))) float2 s_kv[kTab];
-    __shared__ uint32_t s_list[4][CHUNK + 4];
+    __shared__ __attribute__((aligned(16))) float s_kv[kTab];
+    __shared__ float2 s_vis[CHUNK + 1];   // [CHUNK]: zero, for padding visits
+    __shared__ uint2 s_list[4][CHUNK + 4];
     // Per entry: byte 0 = row bands hit, byte 1 = column blocks hit (0 for
     // entries past the chunk); s_pos: table index of the entry's row 0 /
     // column 0 of the tile, + 64 (lo: u, hi: v). With CHUNK = 128 the u
@@ -1346,8 +1350,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     for (int k = t; k < kTab; k += 256)
     {
         s_ku[k] = 0.0f;
-        s_kv[k] = make_float2(0.0f, 0.0f);
+        s_kv[k] = 0.0f;
     }
+    if (t == 0) s_vis[CHUNK] = make_float2(0.0f, 0.0f);
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rw = r;
     if (et < CHUNK && e0 + et < e1)
@@ -1433,15 +1438,14 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 float tv[NTAP];
                 axis_taps<NTAP, true>(p, r.y, v0, v1, tv);
                 const bool neg = ((u0 + v0) & 1) != 0;
-                const float zr = neg ? -r.z : r.z, zi = neg ? -r.w : r.w;
+                s_vis[et] = make_float2(neg ? -r.z : r.z, neg ? -r.w : r.w);
                 float4* q = reinterpret_cast<float4*>(s_kv + eb);
 #pragma unroll
-                for (int d = 0; d + 2 <= NTAP; d += 2)
-                    q[d / 2] = make_float4(tv[d] * zr, tv[d] * zi,
-                            tv[d + 1] * zr, tv[d + 1] * zi);
-                if (NTAP & 1)
-                    s_kv[eb + NTAP - 1] = make_float2(tv[NTAP - 1] * zr,
-                            tv[NTAP - 1] * zi);
+                for (int d = 0; d + 4 <= NTAP; d += 4)
+                    q[d / 4] = make_float4(tv[d], tv[d + 1], tv[d + 2],
+                            tv[d + 3]);
+#pragma unroll
+                for (int d = NTAP & ~3; d < NTAP; ++d) s_kv[eb + d] = tv[d];
             }
         }
         // Next chunk's records, issued after this chunk's last use of r so
@@ -1453,7 +1457,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         }
         lds_barrier();   // B2: entry words and tap tables complete
 
-        uint32_t* list = s_list[wave];
+        uint2* list = s_list[wave];
         // The chunk's entry words, read once for the four column blocks.
         constexpr int kGroups = (CHUNK + 63) / 64;
         uint32_t inf[kGroups], ps[kGroups];
@@ -1481,11 +1485,13 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 const bool hit = (inf[gi] >> wave) & (inf[gi] >> (8 + cblk)) & 1u;
                 const uint64_t m = __ballot(hit);
                 if (hit)
-                    list[cnt + (int)__popcll(m & below)] = ps[gi] + kadd;
+                    list[cnt + (int)__popcll(m & below)] = make_uint2(
+                            ps[gi] + kadd, (uint32_t)(gi * 64 + lane));
                 cnt += (int)__popcll(m);
             }
             const int cnt4 = (cnt + 3) & ~3;
-            if (lane < cnt4 - cnt) list[cnt + lane] = 0u;   // zero visit
+            if (lane < cnt4 - cnt)     // zero visit (zero taps, zero value)
+                list[cnt + lane] = make_uint2(0u, (uint32_t)CHUNK);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
@@ -1494,15 +1500,17 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
             f32x4 re = acc_re[cblk], im = acc_im[cblk];
             for (int g = n16; g < n4; g += 4)
             {
-                const uint32_t w = list[g + kq];
-                const float a = s_ku[(w & 0xffffu) + i];
-                const float2 bb = s_kv[(w >> 16) + i];
+                const uint2 w = list[g + kq];
+                const float a = s_ku[(w.x & 0xffffu) + i];
+                const float kv = s_kv[(w.x >> 16) + i];
+                const float2 z = s_vis[w.y];
+                const float2 bb = make_float2(kv * z.x, kv * z.y);
                 re = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.x, re, 0, 0, 0);
                 im = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.y, im, 0, 0, 0);
             }
             for (int g = 0; g < n16; g += 16)
             {
-                uint32_t w[4];
+                uint2 w[4];
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2) w[s2] = list[g + 4 * s2 + kq];
                 float a[4];
@@ -1510,8 +1518,10 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2)
                 {
-                    a[s2] = s_ku[(w[s2] & 0xffffu) + i];
-                    bb[s2] = s_kv[(w[s2] >> 16) + i];
+                    a[s2] = s_ku[(w[s2].x & 0xffffu) + i];
+                    const float kv = s_kv[(w[s2].x >> 16) + i];
+                    const float2 z = s_vis[w[s2].y];
+                    bb[s2] = make_float2(kv * z.x, kv * z.y);
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2)
