@@ -672,6 +672,7 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
         }
     };
     double prev_median = 0.0;
+    int hpos = 0;                   // t % wmh, the ring slot of step t
     for (int64_t t = 0; t < prm.T; ++t)
     {
         // Opaque per step, so that the per-element address and LDS offset
@@ -720,7 +721,7 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
         }
 
         // Broadband: median history of the last min(t + 1, wmh) steps.
-        if (lane == 0) hist[t % prm.wmh] = median;
+        if (lane == 0) hist[hpos] = median;
         wave_sync();
         const int medwindow = (int)((t + 1 < prm.wmh) ? t + 1 : prm.wmh);
         bool situation = false;
@@ -733,7 +734,10 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
             {
                 const int tt = lane + 64 * j;
                 const bool ok = tt < medwindow;
-                hv[j] = ok ? hist[(t - tt) % prm.wmh] : 0.0;
+                // Ring slot of step t - tt (tt < wmh): no 64-bit modulo.
+                const int slot = hpos - tt < 0 ? hpos - tt + prm.wmh :
+                                                 hpos - tt;
+                hv[j] = ok ? hist[slot] : 0.0;
                 hk[j] = ok ? key_of(hv[j]) : ~(uint64_t)0;
             }
             const int k_h = mid_index(medwindow);
@@ -832,6 +836,7 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
 #pragma unroll
         for (int j = 0; j < EPL; ++j) prev[j] = m[j];
         prev_median = median;
+        hpos = hpos + 1 == prm.wmh ? 0 : hpos + 1;
     }
 }
 
