@@ -911,23 +911,47 @@ __global__ __launch_bounds__(256) void k_bucket_fill2(EsParams<T> p, int nc,
     for (uint32_t e = e0 + t; e < e1; e += 256 * kIn)
     {
         if (!kEarly || e != e0 + t) load(e);
+        // All cursor atomics of the kIn records first, then the stores: a
+        // store right behind its atomic waits for the LDS round trip, and
+        // the next record's atomic behind that store (config 3: level-2
+        // stores 5.6 of 7.1 ms per call with the interleaved form).
+        uint32_t pos[kIn][2][2];
+        bool put[kIn][2][2];
 #pragma unroll
         for (int q = 0; q < kIn; ++q)
         {
-            if (e + q * 256 >= e1) break;
-            int u0, u1, v0, v1, tu0, tu1, tv0, tv1;
-            tap_range(p, rec[q][0], rec[q][1], u0, u1, v0, v1);
-            tile_span<T, MODE>(p, u0, u1, v0, v1, tu0, tu1, tv0, tv1);
-            tu0 = max(tu0, tu_base); tu1 = min(tu1, tu_base + S - 1);
-            tv0 = max(tv0, tv_base); tv1 = min(tv1, tv_base + S - 1);
-            for (int tu = tu0; tu <= tu1; ++tu)
-                for (int tv = tv0; tv <= tv1; ++tv)
+            const bool in = e + q * 256 < e1;
+            int u0, u1, v0, v1, tu0 = 0, tu1 = -1, tv0 = 0, tv1 = -1;
+            if (in)
+            {
+                tap_range(p, rec[q][0], rec[q][1], u0, u1, v0, v1);
+                tile_span<T, MODE>(p, u0, u1, v0, v1, tu0, tu1, tv0, tv1);
+                tu0 = max(tu0, tu_base); tu1 = min(tu1, tu_base + S - 1);
+                tv0 = max(tv0, tv_base); tv1 = min(tv1, tv_base + S - 1);
+            }
+            // A support spans at most 2 tiles per axis.
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
                 {
-                    const int j = ((tu - tu_base) << p.sshift) | (tv - tv_base);
-                    const uint32_t pos = atomicAdd(&cur[j], 1u);
-                    store_rec<T, kWords>(recs + (size_t)pos * kWords, rec[q]);
+                    const int tu = tu0 + a, tv = tv0 + b;
+                    put[q][a][b] = tu <= tu1 && tv <= tv1;
+                    pos[q][a][b] = 0;
+                    if (put[q][a][b])
+                        pos[q][a][b] = atomicAdd(&cur[((tu - tu_base) <<
+                                p.sshift) | (tv - tv_base)], 1u);
                 }
         }
+#pragma unroll
+        for (int q = 0; q < kIn; ++q)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+                    if (put[q][a][b])
+                        store_rec<T, kWords>(recs + (size_t)pos[q][a][b] *
+                                kWords, rec[q]);
     }
 }
 
