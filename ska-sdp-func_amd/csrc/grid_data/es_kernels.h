@@ -1,17 +1,19 @@
 // HIP kernels of the MI355X-native ES-FFT (de)gridder: launch interface.
 //
-// Data path (one w-plane, one call):
-//   bucket_count -> scan_columns -> scan_bins -> bucket_fill -> (grid) zero_hot_tiles + scatter_tiles
-//                     (degrid) gather_tiles
+// Data path (one call; 3-D: one bucketing for every w-plane):
+//   bucket_count -> scan_columns -> bucket_fill1 (+ scan_bins in its last
+//   block) -> bucket_fill2 -> (grid) zero_shared_tiles + scatter_tab
+//                             (degrid) gather_win
 // Visibilities are bucketed by 64x64 grid tile (counting sort, LDS-private
 // histograms per chunk of visibilities; records move in two levels: by
-// super bin of S x S tiles with LDS-staged coalesced stores, then by tile). In grid mode a visibility is listed
-// in every tile its support touches and each tile only accumulates the taps
-// that fall inside it, so every grid cell has exactly one owning workgroup:
-// the tile is accumulated in LDS (ds_add) and written to HBM ONCE with plain
-// stores (no global atomics, no separate memset of the grid). Tiles with
-// more entries than one work item takes are split into pieces that combine
-// with global float atomics into a tile zeroed beforehand.
+// super bin of S x S tiles with LDS-staged coalesced stores, then by tile).
+// In grid mode a visibility is listed in every tile its support touches and
+// each tile only accumulates the taps that fall inside it, so every grid
+// cell has exactly one owning workgroup: the tile is accumulated in matrix-
+// core accumulators and written to HBM ONCE with plain stores (no global
+// atomics, no separate memset of the grid). Tiles with more entries than
+// one work item takes are split into pieces that combine with global float
+// atomics into a tile zeroed beforehand.
 #ifndef SDP_ES_KERNELS_H_
 #define SDP_ES_KERNELS_H_
 

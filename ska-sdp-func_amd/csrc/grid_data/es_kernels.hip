@@ -458,7 +458,19 @@ __device__ __forceinline__ void block_scan_1024(uint32_t& a, uint32_t& b,
     __syncthreads();
 }
 
-__global__ __launch_bounds__(1024) void k_scan_bins(
+// Run by one 1024-thread block: the extra last block of k_bucket_fill1
+// (round 5; it was its own single-block launch, 12.5 us at config 2,
+// serial between the column scans and level 1).
+struct ScanBinsArgs
+{
+    uint32_t* bin_start;
+    uint32_t* item_start;
+    uint32_t* totals;
+    uint32_t* item_bin;
+    uint32_t item_capacity;
+};
+
+__device__ __forceinline__ void scan_bins_block(
         const uint32_t* __restrict__ bin_count, int nbins,
         uint32_t* __restrict__ bin_start, uint32_t* __restrict__ item_start,
         uint32_t* __restrict__ totals, uint32_t* __restrict__ item_bin,
@@ -678,8 +690,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(
         const T* __restrict__ freq, const T* __restrict__ vis,
         const T* __restrict__ weight, const uint32_t* __restrict__ stable,
         const uint32_t* __restrict__ bin_count, uint32_t* __restrict__ sb_start,
-        T* __restrict__ recs1)
+        T* __restrict__ recs1, ScanBinsArgs sba)
 {
+    static_assert(NT == 1024, "the extra block runs scan_bins_block");
+    if (blockIdx.x == gridDim.x - 1)
+    {
+        // Tile-bin / work-item prefix for level 2 and the tile kernels: it
+        // needs only the column scans, so it runs beside level 1.
+        scan_bins_block(bin_count, p.nbins, sba.bin_start, sba.item_start,
+                sba.totals, sba.item_bin, sba.item_capacity);
+        return;
+    }
     constexpr int kWords = Rec<T, MODE, DO_W>::kWords;
     constexpr int K = Fill1Shape<T, kWords>::K;
     constexpr int kBatch = NT * K;
@@ -2506,9 +2527,11 @@ int launch_fill(int nc, int64_t chunk, const EsParams<T>& p,
         const T* vis, const T* weight, const BucketScratch* s,
         const uint32_t* stable, uint32_t* gtable, hipStream_t stream)
 {
-    k_bucket_fill1<T, MODE, DO_W, NT><<<nc, NT, 0, stream>>>(p, num_rows,
+    const ScanBinsArgs sba{s->bin_start, s->item_start, s->totals,
+            s->item_bin, s->item_capacity};
+    k_bucket_fill1<T, MODE, DO_W, NT><<<nc + 1, NT, 0, stream>>>(p, num_rows,
             num_chan, chunk, uvw, freq, vis, weight, stable, s->bin_count,
-            s->sb_start, (T*)s->recs1);
+            s->sb_start, (T*)s->recs1, sba);
     // Chunk groups x super bins: each block moves the records of one
     // group of kGroupChunks chunks of one super bin.
     const int ng = (nc + kGroupChunks - 1) / kGroupChunks;
@@ -2587,10 +2610,6 @@ int bucket(const EsParams<T>& p_in, Mode mode, int64_t num_rows, int num_chan,
     const int gblk = (p.nbins + 63) / 64, sblk = (p.nsbins + 63) / 64;
     k_scan_columns<<<gblk + sblk, 1024, 0, stream>>>(gtable, ng, p.nbins,
             s->bin_count, gblk, stable, nc, p.nsbins, s->bin_count + p.nbins);
-    SDP_HIP_CHECK_LAUNCH(status);
-    k_scan_bins<<<1, 1024, 0, stream>>>(s->bin_count, p.nbins,
-            s->bin_start, s->item_start, s->totals, s->item_bin,
-            s->item_capacity);
     SDP_HIP_CHECK_LAUNCH(status);
     // No host round trip: records and work items are sized for the worst
     // case by the caller (BucketScratch::recs_bytes / item_capacity).
