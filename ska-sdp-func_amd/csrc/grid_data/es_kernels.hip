@@ -162,6 +162,21 @@ __device__ __forceinline__ bool footprint(const EsParams<T>& p, T u, T v,
 // coordinate pos_w, footprint() with p.plane < 0): the same arithmetic as
 // footprint(); false (tap 0) if the visibility does not touch the plane.
 template<typename T>
+__device__ __forceinline__ bool plane_tap_at(const EsParams<T>& p, int plane,
+        T pos_w, T& kw)
+{
+#pragma clang fp contract(off)
+    const T half_support = T(p.support) / T(2);
+    const int w0 = (int)ceil(pos_w - half_support);
+    const int w1 = (int)floor(pos_w + half_support);
+    kw = T(0);
+    if (plane < w0 || plane > w1) return false;
+    const T inv_half_support = T(1) / half_support;
+    kw = es_tap(p.beta, (T)(plane - pos_w) * inv_half_support);
+    return true;
+}
+
+template<typename T>
 __device__ __forceinline__ bool plane_tap(const EsParams<T>& p, T pos_w,
         T& kw)
 {
@@ -1524,13 +1539,18 @@ __device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
 // of 4 (tile kernel 0.461 -> 0.447 ms at config 2, 26.1 -> 25.3 ms at
 // config 3, 4.42 -> 4.24 ms for 10 w-planes).
 constexpr int kScatterChunk = 128;
-template<bool DO_W, int NTAP, int CHUNK = kScatterChunk>
+// PLANES = 2 (3-D): w-planes p.plane and plane2 in one pass: the entries'
+// u / v taps, lists and operand reads are shared, each visit feeds both
+// planes' accumulators (visibility x w-tap of each plane), and the tile
+// is written to grid and grid2.
+template<bool DO_W, int NTAP, int CHUNK = kScatterChunk, int PLANES = 1>
 __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
         const uint32_t* __restrict__ item_bin, float* __restrict__ grid,
-        int flags)
+        int flags, float* __restrict__ grid2 = nullptr, int plane2 = 0)
 {
+    static_assert(PLANES == 1 || (PLANES == 2 && DO_W), "two planes: 3-D");
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     static_assert(CHUNK == 256 || (CHUNK <= 128 && CHUNK % 16 == 0),
             "one or two threads per entry");
@@ -1544,6 +1564,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     __shared__ __attribute__((aligned(16))) float s_ku[kTab];
     __shared__ __attribute__((aligned(16))) float s_kv[kTab];
     __shared__ float2 s_vis[CHUNK + 1];   // [CHUNK]: zero, for padding visits
+    __shared__ float2 s_vis2[PLANES == 2 ? CHUNK + 1 : 1];
     __shared__ uint2 s_list[4][CHUNK + 4];
     // Per entry: byte 0 = row bands hit, byte 1 = column blocks hit (0 for
     // entries past the chunk); s_pos: table index of the entry's row 0 /
@@ -1578,18 +1599,28 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     const bool stage_u = CHUNK == 256 || t < 128;
     const bool stage_v = CHUNK == 256 || t >= 128;
     f32x4 acc_re[4], acc_im[4];
+    f32x4 acc_re2[PLANES == 2 ? 4 : 1], acc_im2[PLANES == 2 ? 4 : 1];
 #pragma unroll
     for (int cblk = 0; cblk < 4; ++cblk)
     {
         acc_re[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         acc_im[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        if constexpr (PLANES == 2)
+        {
+            acc_re2[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            acc_im2[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
     }
     for (int k = t; k < kTab; k += 256)
     {
         s_ku[k] = 0.0f;
         s_kv[k] = 0.0f;
     }
-    if (t == 0) s_vis[CHUNK] = make_float2(0.0f, 0.0f);
+    if (t == 0)
+    {
+        s_vis[CHUNK] = make_float2(0.0f, 0.0f);
+        if constexpr (PLANES == 2) s_vis2[CHUNK] = make_float2(0.0f, 0.0f);
+    }
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rw = r;
     if (et < CHUNK && e0 + et < e1)
@@ -1609,6 +1640,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         uint32_t rm = 0, cm = 0, pu16 = 0, pv16 = 0;
         const int eb = kLead + et * kStride;
         bool on_plane = live;
+        float vz2r = 0.0f, vz2i = 0.0f;   // PLANES == 2: w V on plane2
         {
 #pragma clang fp contract(off)
             if (DO_W)
@@ -1617,6 +1649,14 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 // an entry off this w-plane gets no visits.
                 float kw = 0.0f;
                 on_plane = live && plane_tap(p, rw.x, kw);
+                if constexpr (PLANES == 2)
+                {
+                    float kw2 = 0.0f;
+                    on_plane = (live && plane_tap_at(p, plane2, rw.x, kw2)) ||
+                            on_plane;
+                    vz2r = r.z * kw2;
+                    vz2i = r.w * kw2;
+                }
                 r.z *= kw;
                 r.w *= kw;
             }
@@ -1676,6 +1716,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 axis_taps<NTAP, true>(p, r.y, v0, v1, tv);
                 const bool neg = ((u0 + v0) & 1) != 0;
                 s_vis[et] = make_float2(neg ? -r.z : r.z, neg ? -r.w : r.w);
+                if constexpr (PLANES == 2)
+                    s_vis2[et] = make_float2(neg ? -vz2r : vz2r,
+                            neg ? -vz2i : vz2i);
                 float4* q = reinterpret_cast<float4*>(s_kv + eb);
 #pragma unroll
                 for (int d = 0; d + 4 <= NTAP; d += 4)
@@ -1735,6 +1778,12 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
             const int n4 = __builtin_amdgcn_readfirstlane(cnt4);
             const int n16 = n4 & ~15;
             f32x4 re = acc_re[cblk], im = acc_im[cblk];
+            f32x4 re2, im2;
+            if constexpr (PLANES == 2)
+            {
+                re2 = acc_re2[cblk];
+                im2 = acc_im2[cblk];
+            }
             for (int g = n16; g < n4; g += 4)
             {
                 const uint2 w = list[g + kq];
@@ -1744,6 +1793,14 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 const float2 bb = make_float2(kv * z.x, kv * z.y);
                 re = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.x, re, 0, 0, 0);
                 im = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.y, im, 0, 0, 0);
+                if constexpr (PLANES == 2)
+                {
+                    const float2 z2 = s_vis2[w.y];
+                    re2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, kv * z2.x,
+                            re2, 0, 0, 0);
+                    im2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, kv * z2.y,
+                            im2, 0, 0, 0);
+                }
             }
             for (int g = 0; g < n16; g += 16)
             {
@@ -1752,6 +1809,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 for (int s2 = 0; s2 < 4; ++s2) w[s2] = list[g + 4 * s2 + kq];
                 float a[4];
                 float2 bb[4];
+                float2 bb2[PLANES == 2 ? 4 : 1];
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2)
                 {
@@ -1759,6 +1817,11 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                     const float kv = s_kv[(w[s2].x >> 16) + i];
                     const float2 z = s_vis[w[s2].y];
                     bb[s2] = make_float2(kv * z.x, kv * z.y);
+                    if constexpr (PLANES == 2)
+                    {
+                        const float2 z2 = s_vis2[w[s2].y];
+                        bb2[s2] = make_float2(kv * z2.x, kv * z2.y);
+                    }
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2)
@@ -1768,48 +1831,69 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 for (int s2 = 0; s2 < 4; ++s2)
                     im = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], bb[s2].y,
                             im, 0, 0, 0);
+                if constexpr (PLANES == 2)
+                {
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2)
+                        re2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2],
+                                bb2[s2].x, re2, 0, 0, 0);
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2)
+                        im2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2],
+                                bb2[s2].y, im2, 0, 0, 0);
+                }
             }
             acc_re[cblk] = re;
             acc_im[cblk] = im;
+            if constexpr (PLANES == 2)
+            {
+                acc_re2[cblk] = re2;
+                acc_im2[cblk] = im2;
+            }
             // The list is rebuilt for the next column block.
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
         }
     }
+    auto write_tile = [&](float* __restrict__ g, const f32x4 (&ar)[4],
+            const f32x4 (&ai)[4]) {
 #pragma unroll
-    for (int cblk = 0; cblk < 4; ++cblk)
-    {
-        const int col = c0 + cblk * 16 + i;
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr)
+        for (int cblk = 0; cblk < 4; ++cblk)
         {
-            const int row = r0 + sub_r + kq * 4 + rr;
-            if (row >= p.G || col >= p.G) continue;
-            float* dst = grid + ((size_t)row * p.G + col) * 2;
-            if (npieces == 1 && accumulate)
+            const int col = c0 + cblk * 16 + i;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
             {
-                float2 v = *(const float2*)dst;
-                v.x += acc_re[cblk][rr];
-                v.y += acc_im[cblk][rr];
-                *(float2*)dst = v;
-            }
-            else if (npieces == 1)
-            {
-                float2 v;
-                v.x = acc_re[cblk][rr];
-                v.y = acc_im[cblk][rr];
-                *(float2*)dst = v;
-            }
-            else
-            {
-                if (acc_re[cblk][rr] != 0.0f)
-                    unsafeAtomicAdd(dst, acc_re[cblk][rr]);
-                if (acc_im[cblk][rr] != 0.0f)
-                    unsafeAtomicAdd(dst + 1, acc_im[cblk][rr]);
+                const int row = r0 + sub_r + kq * 4 + rr;
+                if (row >= p.G || col >= p.G) continue;
+                float* dst = g + ((size_t)row * p.G + col) * 2;
+                if (npieces == 1 && accumulate)
+                {
+                    float2 v = *(const float2*)dst;
+                    v.x += ar[cblk][rr];
+                    v.y += ai[cblk][rr];
+                    *(float2*)dst = v;
+                }
+                else if (npieces == 1)
+                {
+                    float2 v;
+                    v.x = ar[cblk][rr];
+                    v.y = ai[cblk][rr];
+                    *(float2*)dst = v;
+                }
+                else
+                {
+                    if (ar[cblk][rr] != 0.0f)
+                        unsafeAtomicAdd(dst, ar[cblk][rr]);
+                    if (ai[cblk][rr] != 0.0f)
+                        unsafeAtomicAdd(dst + 1, ai[cblk][rr]);
+                }
             }
         }
-    }
+    };
+    write_tile(grid, acc_re, acc_im);
+    if constexpr (PLANES == 2) write_tile(grid2, acc_re2, acc_im2);
 }
 
 // Degrid mode, f32, matrix-core form with per-entry tap tables (the hot
@@ -2708,6 +2792,40 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     return *status;
 }
 
+// 3-D, f32, W <= 8: w-planes p.plane and plane2 (into grid2) in one pass
+// of the tile kernel (k_scatter_tab<.., 2>): the staging, visit lists and
+// operand reads of the entries are shared by the two planes.
+template<typename T>
+bool two_plane_scatter_ok(const EsParams<T>& p)
+{
+    return sizeof(T) == 4 && p.do_w && p.support <= 8;
+}
+
+template<typename T>
+int scatter_two_planes(const EsParams<T>& p, const BucketScratch& s,
+        uint32_t n_items, T* grid, int plane2, T* grid2, hipStream_t stream,
+        bool skip_empty)
+{
+    sdp_Error st = SDP_SUCCESS;
+    sdp_Error* status = &st;
+    if (!two_plane_scatter_ok(p)) return SDP_ERR_RUNTIME;
+    if constexpr (sizeof(T) == 4)
+    {
+        k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
+                p, s.item_start, grid);
+        SDP_HIP_CHECK_LAUNCH(status);
+        k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
+                p, s.item_start, grid2);
+        SDP_HIP_CHECK_LAUNCH(status);
+        const int se = skip_empty ? 1 : 0;
+        k_scatter_tab<true, 9, kScatterChunk, 2><<<n_items, 256, 0, stream>>>(
+                p, (const float*)s.recs, s.bin_start, s.item_start,
+                s.item_bin, grid, se, grid2, plane2);
+        SDP_HIP_CHECK_LAUNCH(status);
+    }
+    return *status;
+}
+
 // f32: W <= 8 the lane-per-entry window gather (k_gather_win), W = 16 the
 // matrix-core sub-tile form (k_gather_tab); f64: the LDS window gather.
 template<typename T>
@@ -2825,6 +2943,9 @@ int reverse_screen(const ImageParams<T>& ip, int plane, T* dirty,
             uint32_t*, uint32_t*); \
     template int scatter<T>(const EsParams<T>&, const BucketScratch&, \
             uint32_t, T*, hipStream_t, bool, bool); \
+    template bool two_plane_scatter_ok<T>(const EsParams<T>&); \
+    template int scatter_two_planes<T>(const EsParams<T>&, \
+            const BucketScratch&, uint32_t, T*, int, T*, hipStream_t, bool); \
     template int gather<T>(const EsParams<T>&, const BucketScratch&, \
             uint32_t, const T*, T*, hipStream_t); \
     template int screen_corr_2d<T>(const ImageParams<T>&, const T*, T*, \

@@ -51,6 +51,7 @@ struct sdp_GridderUvwEsFft
 
     // Device state.
     void* grid;                 // G x G complex plane
+    void* grid2;                // second plane (3-D two-plane tile passes)
     void* tables;               // conv_corr | quad kernel | nodes | weights
     int ntiles;
     int ncoarse;
@@ -498,12 +499,50 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
         timing_mark(plan, 1);
         timing_collect_range(plan, 0, 1, kGridSlots);
     }
-    for (int plane = 0; plane < plan->num_total_w_grids && !*status; ++plane)
+    const int nplanes = plan->num_total_w_grids;
+    for (int plane = 0; plane < nplanes && !*status; ++plane)
     {
         if (batched)
         {
             scatter_batches<T>(plan, plane, rows, rb, chan, uvw, freq, vis,
                     weight, grid, status);
+        }
+        else if (plane + 1 < nplanes &&
+                sdp_es::two_plane_scatter_ok(es_params<T>(plan, plane)))
+        {
+            // 3-D: this plane and the next in one tile-kernel pass (the
+            // entries' staging is shared), the next one into grid2.
+            if (!plan->grid2)
+            {
+                const size_t cells = (size_t)plan->grid_size *
+                        plan->grid_size;
+                SDP_HIP_CHECK(hipMalloc(&plan->grid2, cells * 2 * sizeof(T)),
+                        status);
+                if (*status) return;
+            }
+            T* grid2 = (T*)plan->grid2;
+            timing_mark(plan, 1);
+            int e = sdp_es::scatter_two_planes<T>(es_params<T>(plan, plane),
+                    plan->scratch, n_items, grid, plane + 1, grid2,
+                    plan->stream, sparse);
+            if (e) { *status = (sdp_Error)e; return; }
+            timing_mark(plan, 2);
+            grid_to_image<T>(plan, ip, plane, grid, dirty, sparse, status);
+            if (*status) return;
+            timing_mark(plan, 4);
+            timing_collect_range(plan, 1, 4, kGridSlots);
+            ++plane;
+            timing_mark(plan, 2);
+            grid_to_image<T>(plan, ip, plane, grid2, dirty, sparse, status);
+            if (*status) return;
+            if (plane == nplanes - 1)
+            {
+                e = sdp_es::apply_correction<T>(ip, dirty, plan->stream);
+                if (e) { *status = (sdp_Error)e; return; }
+            }
+            timing_mark(plan, 4);
+            timing_collect_range(plan, 2, 4, kGridSlots);
+            continue;
         }
         else
         {
@@ -632,6 +671,7 @@ void sdp_gridder_uvw_es_fft_free_plan(sdp_GridderUvwEsFft* plan)
 {
     if (!plan) return;
     if (plan->grid) (void)hipFree(plan->grid);
+    if (plan->grid2) (void)hipFree(plan->grid2);
     if (plan->tables) (void)hipFree(plan->tables);
     sdp_es::BucketScratch& s = plan->scratch;
     if (s.table) (void)hipFree(s.table);
