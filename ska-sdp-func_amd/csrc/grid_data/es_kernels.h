@@ -139,13 +139,14 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
         T* grid, hipStream_t stream, bool skip_empty = false,
         bool accumulate = false);
 
-// 3-D, f32, W <= 8: planes p.plane (into grid) and plane2 (into grid2) in
-// one tile-kernel pass (skip_empty as scatter; no accumulate form).
+// 3-D, f32, W <= 8: planes p.plane .. p.plane + nplanes - 1 (into
+// grids[0..nplanes), 2 <= nplanes <= planes_per_pass(p)) in one tile-kernel
+// pass (skip_empty as scatter; no accumulate form).
 template<typename T>
-bool two_plane_scatter_ok(const EsParams<T>& p);
+int planes_per_pass(const EsParams<T>& p);
 template<typename T>
-int scatter_two_planes(const EsParams<T>& p, const BucketScratch& s,
-        uint32_t n_items, T* grid, int plane2, T* grid2, hipStream_t stream,
+int scatter_planes(const EsParams<T>& p, const BucketScratch& s,
+        uint32_t n_items, T* const* grids, int nplanes, hipStream_t stream,
         bool skip_empty);
 
 // Degrid-mode tile gather: vis[idx] += sum_taps grid * kernel.

@@ -1539,6 +1539,9 @@ __device__ __forceinline__ void pool_layout(const PoolCounts<kNS>& pc,
 // of 4 (tile kernel 0.461 -> 0.447 ms at config 2, 26.1 -> 25.3 ms at
 // config 3, 4.42 -> 4.24 ms for 10 w-planes).
 constexpr int kScatterChunk = 128;
+// w-planes per 3-D tile-kernel pass: 2 (10 planes: 1076 -> 1165 Mvis/s);
+// 3 measured 1134 (162 VGPRs, 3 waves per SIMD, and a lone tenth plane).
+constexpr int kScatterPlanes = 2;
 // PLANES = 2 (3-D): w-planes p.plane and plane2 in one pass: the entries'
 // u / v taps, lists and operand reads are shared, each visit feeds both
 // planes' accumulators (visibility x w-tap of each plane), and the tile
@@ -1548,9 +1551,13 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         const float* __restrict__ recs, const uint32_t* __restrict__ bin_start,
         const uint32_t* __restrict__ item_start,
         const uint32_t* __restrict__ item_bin, float* __restrict__ grid,
-        int flags, float* __restrict__ grid2 = nullptr, int plane2 = 0)
+        int flags, float* __restrict__ grid2 = nullptr, int plane2 = 0,
+        float* __restrict__ grid3 = nullptr)
 {
-    static_assert(PLANES == 1 || (PLANES == 2 && DO_W), "two planes: 3-D");
+    static_assert(PLANES == 1 || (PLANES <= 3 && DO_W), "planes 2, 3: 3-D");
+    // (PLANES = 3 compiles and passed the 3-D tests, but loses: see
+    // kScatterPlanes.)
+    constexpr int kX = PLANES > 1 ? PLANES - 1 : 1;   // extra planes
     using f32x4 = __attribute__((ext_vector_type(4))) float;
     static_assert(CHUNK == 256 || (CHUNK <= 128 && CHUNK % 16 == 0),
             "one or two threads per entry");
@@ -1564,7 +1571,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     __shared__ __attribute__((aligned(16))) float s_ku[kTab];
     __shared__ __attribute__((aligned(16))) float s_kv[kTab];
     __shared__ float2 s_vis[CHUNK + 1];   // [CHUNK]: zero, for padding visits
-    __shared__ float2 s_vis2[PLANES == 2 ? CHUNK + 1 : 1];
+    __shared__ float2 s_visx[kX][PLANES > 1 ? CHUNK + 1 : 1];
     __shared__ uint2 s_list[4][CHUNK + 4];
     // Per entry: byte 0 = row bands hit, byte 1 = column blocks hit (0 for
     // entries past the chunk); s_pos: table index of the entry's row 0 /
@@ -1599,17 +1606,19 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     const bool stage_u = CHUNK == 256 || t < 128;
     const bool stage_v = CHUNK == 256 || t >= 128;
     f32x4 acc_re[4], acc_im[4];
-    f32x4 acc_re2[PLANES == 2 ? 4 : 1], acc_im2[PLANES == 2 ? 4 : 1];
+    f32x4 acc_rex[kX][PLANES > 1 ? 4 : 1], acc_imx[kX][PLANES > 1 ? 4 : 1];
 #pragma unroll
     for (int cblk = 0; cblk < 4; ++cblk)
     {
         acc_re[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         acc_im[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        if constexpr (PLANES == 2)
-        {
-            acc_re2[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-            acc_im2[cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
+        if constexpr (PLANES > 1)
+#pragma unroll
+            for (int x = 0; x < kX; ++x)
+            {
+                acc_rex[x][cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+                acc_imx[x][cblk] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+            }
     }
     for (int k = t; k < kTab; k += 256)
     {
@@ -1619,7 +1628,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     if (t == 0)
     {
         s_vis[CHUNK] = make_float2(0.0f, 0.0f);
-        if constexpr (PLANES == 2) s_vis2[CHUNK] = make_float2(0.0f, 0.0f);
+        if constexpr (PLANES > 1)
+            for (int x = 0; x < kX; ++x)
+                s_visx[x][CHUNK] = make_float2(0.0f, 0.0f);
     }
     const float4* recs4 = (const float4*)recs;
     float4 r = make_float4(0.0f, 0.0f, 0.0f, 0.0f), rw = r;
@@ -1640,7 +1651,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         uint32_t rm = 0, cm = 0, pu16 = 0, pv16 = 0;
         const int eb = kLead + et * kStride;
         bool on_plane = live;
-        float vz2r = 0.0f, vz2i = 0.0f;   // PLANES == 2: w V on plane2
+        float vxr[kX], vxi[kX];           // w V on the extra planes
         {
 #pragma clang fp contract(off)
             if (DO_W)
@@ -1649,14 +1660,16 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 // an entry off this w-plane gets no visits.
                 float kw = 0.0f;
                 on_plane = live && plane_tap(p, rw.x, kw);
-                if constexpr (PLANES == 2)
-                {
-                    float kw2 = 0.0f;
-                    on_plane = (live && plane_tap_at(p, plane2, rw.x, kw2)) ||
-                            on_plane;
-                    vz2r = r.z * kw2;
-                    vz2i = r.w * kw2;
-                }
+                if constexpr (PLANES > 1)
+#pragma unroll
+                    for (int x = 0; x < kX; ++x)
+                    {
+                        float kw2 = 0.0f;
+                        on_plane = (live && plane_tap_at(p, plane2 + x, rw.x,
+                                kw2)) || on_plane;
+                        vxr[x] = r.z * kw2;
+                        vxi[x] = r.w * kw2;
+                    }
                 r.z *= kw;
                 r.w *= kw;
             }
@@ -1716,9 +1729,11 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 axis_taps<NTAP, true>(p, r.y, v0, v1, tv);
                 const bool neg = ((u0 + v0) & 1) != 0;
                 s_vis[et] = make_float2(neg ? -r.z : r.z, neg ? -r.w : r.w);
-                if constexpr (PLANES == 2)
-                    s_vis2[et] = make_float2(neg ? -vz2r : vz2r,
-                            neg ? -vz2i : vz2i);
+                if constexpr (PLANES > 1)
+#pragma unroll
+                    for (int x = 0; x < kX; ++x)
+                        s_visx[x][et] = make_float2(neg ? -vxr[x] : vxr[x],
+                                neg ? -vxi[x] : vxi[x]);
                 float4* q = reinterpret_cast<float4*>(s_kv + eb);
 #pragma unroll
                 for (int d = 0; d + 4 <= NTAP; d += 4)
@@ -1778,12 +1793,14 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
             const int n4 = __builtin_amdgcn_readfirstlane(cnt4);
             const int n16 = n4 & ~15;
             f32x4 re = acc_re[cblk], im = acc_im[cblk];
-            f32x4 re2, im2;
-            if constexpr (PLANES == 2)
-            {
-                re2 = acc_re2[cblk];
-                im2 = acc_im2[cblk];
-            }
+            f32x4 rex[kX], imx[kX];
+            if constexpr (PLANES > 1)
+#pragma unroll
+                for (int x = 0; x < kX; ++x)
+                {
+                    rex[x] = acc_rex[x][cblk];
+                    imx[x] = acc_imx[x][cblk];
+                }
             for (int g = n16; g < n4; g += 4)
             {
                 const uint2 w = list[g + kq];
@@ -1793,14 +1810,16 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 const float2 bb = make_float2(kv * z.x, kv * z.y);
                 re = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.x, re, 0, 0, 0);
                 im = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.y, im, 0, 0, 0);
-                if constexpr (PLANES == 2)
-                {
-                    const float2 z2 = s_vis2[w.y];
-                    re2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, kv * z2.x,
-                            re2, 0, 0, 0);
-                    im2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, kv * z2.y,
-                            im2, 0, 0, 0);
-                }
+                if constexpr (PLANES > 1)
+#pragma unroll
+                    for (int x = 0; x < kX; ++x)
+                    {
+                        const float2 z2 = s_visx[x][w.y];
+                        rex[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a,
+                                kv * z2.x, rex[x], 0, 0, 0);
+                        imx[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a,
+                                kv * z2.y, imx[x], 0, 0, 0);
+                    }
             }
             for (int g = 0; g < n16; g += 16)
             {
@@ -1809,7 +1828,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 for (int s2 = 0; s2 < 4; ++s2) w[s2] = list[g + 4 * s2 + kq];
                 float a[4];
                 float2 bb[4];
-                float2 bb2[PLANES == 2 ? 4 : 1];
+                float2 bbx[kX][PLANES > 1 ? 4 : 1];
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2)
                 {
@@ -1817,11 +1836,13 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                     const float kv = s_kv[(w[s2].x >> 16) + i];
                     const float2 z = s_vis[w[s2].y];
                     bb[s2] = make_float2(kv * z.x, kv * z.y);
-                    if constexpr (PLANES == 2)
-                    {
-                        const float2 z2 = s_vis2[w[s2].y];
-                        bb2[s2] = make_float2(kv * z2.x, kv * z2.y);
-                    }
+                    if constexpr (PLANES > 1)
+#pragma unroll
+                        for (int x = 0; x < kX; ++x)
+                        {
+                            const float2 z2 = s_visx[x][w[s2].y];
+                            bbx[x][s2] = make_float2(kv * z2.x, kv * z2.y);
+                        }
                 }
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2)
@@ -1831,25 +1852,29 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 for (int s2 = 0; s2 < 4; ++s2)
                     im = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2], bb[s2].y,
                             im, 0, 0, 0);
-                if constexpr (PLANES == 2)
-                {
+                if constexpr (PLANES > 1)
 #pragma unroll
-                    for (int s2 = 0; s2 < 4; ++s2)
-                        re2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2],
-                                bb2[s2].x, re2, 0, 0, 0);
+                    for (int x = 0; x < kX; ++x)
+                    {
 #pragma unroll
-                    for (int s2 = 0; s2 < 4; ++s2)
-                        im2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s2],
-                                bb2[s2].y, im2, 0, 0, 0);
-                }
+                        for (int s2 = 0; s2 < 4; ++s2)
+                            rex[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                                    a[s2], bbx[x][s2].x, rex[x], 0, 0, 0);
+#pragma unroll
+                        for (int s2 = 0; s2 < 4; ++s2)
+                            imx[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                                    a[s2], bbx[x][s2].y, imx[x], 0, 0, 0);
+                    }
             }
             acc_re[cblk] = re;
             acc_im[cblk] = im;
-            if constexpr (PLANES == 2)
-            {
-                acc_re2[cblk] = re2;
-                acc_im2[cblk] = im2;
-            }
+            if constexpr (PLANES > 1)
+#pragma unroll
+                for (int x = 0; x < kX; ++x)
+                {
+                    acc_rex[x][cblk] = rex[x];
+                    acc_imx[x][cblk] = imx[x];
+                }
             // The list is rebuilt for the next column block.
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
             __builtin_amdgcn_wave_barrier();
@@ -1893,7 +1918,8 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         }
     };
     write_tile(grid, acc_re, acc_im);
-    if constexpr (PLANES == 2) write_tile(grid2, acc_re2, acc_im2);
+    if constexpr (PLANES > 1) write_tile(grid2, acc_rex[0], acc_imx[0]);
+    if constexpr (PLANES > 2) write_tile(grid3, acc_rex[1], acc_imx[1]);
 }
 
 // Degrid mode, f32, matrix-core form with per-entry tap tables (the hot
@@ -2792,35 +2818,38 @@ int scatter(const EsParams<T>& p, const BucketScratch& s, uint32_t n_items,
     return *status;
 }
 
-// 3-D, f32, W <= 8: w-planes p.plane and plane2 (into grid2) in one pass
-// of the tile kernel (k_scatter_tab<.., 2>): the staging, visit lists and
-// operand reads of the entries are shared by the two planes.
+// 3-D, f32, W <= 8: w-planes p.plane .. p.plane + nplanes - 1 (into
+// grids[0..nplanes)) in one pass of the tile kernel (k_scatter_tab<.., 2 or
+// 3>): the staging, visit lists and operand reads of the entries are shared
+// by the planes.
 template<typename T>
-bool two_plane_scatter_ok(const EsParams<T>& p)
+int planes_per_pass(const EsParams<T>& p)
 {
-    return sizeof(T) == 4 && p.do_w && p.support <= 8;
+    return (sizeof(T) == 4 && p.do_w && p.support <= 8) ? kScatterPlanes : 1;
 }
 
 template<typename T>
-int scatter_two_planes(const EsParams<T>& p, const BucketScratch& s,
-        uint32_t n_items, T* grid, int plane2, T* grid2, hipStream_t stream,
+int scatter_planes(const EsParams<T>& p, const BucketScratch& s,
+        uint32_t n_items, T* const* grids, int nplanes, hipStream_t stream,
         bool skip_empty)
 {
     sdp_Error st = SDP_SUCCESS;
     sdp_Error* status = &st;
-    if (!two_plane_scatter_ok(p)) return SDP_ERR_RUNTIME;
+    if (nplanes < 2 || nplanes > planes_per_pass(p)) return SDP_ERR_RUNTIME;
     if constexpr (sizeof(T) == 4)
     {
-        k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
-                p, s.item_start, grid);
-        SDP_HIP_CHECK_LAUNCH(status);
-        k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
-                p, s.item_start, grid2);
-        SDP_HIP_CHECK_LAUNCH(status);
+        for (int q = 0; q < nplanes; ++q)
+        {
+            k_zero_shared_tiles<T><<<p.nbins, kThreads, 0, stream>>>(
+                    p, s.item_start, grids[q]);
+            SDP_HIP_CHECK_LAUNCH(status);
+        }
         const int se = skip_empty ? 1 : 0;
-        k_scatter_tab<true, 9, kScatterChunk, 2><<<n_items, 256, 0, stream>>>(
-                p, (const float*)s.recs, s.bin_start, s.item_start,
-                s.item_bin, grid, se, grid2, plane2);
+        const float* recs = (const float*)s.recs;
+        static_assert(kScatterPlanes == 2, "one multi-plane kernel");
+        k_scatter_tab<true, 9, kScatterChunk, kScatterPlanes><<<n_items, 256,
+                0, stream>>>(p, recs, s.bin_start, s.item_start, s.item_bin,
+                grids[0], se, grids[1], p.plane + 1);
         SDP_HIP_CHECK_LAUNCH(status);
     }
     return *status;
@@ -2943,9 +2972,10 @@ int reverse_screen(const ImageParams<T>& ip, int plane, T* dirty,
             uint32_t*, uint32_t*); \
     template int scatter<T>(const EsParams<T>&, const BucketScratch&, \
             uint32_t, T*, hipStream_t, bool, bool); \
-    template bool two_plane_scatter_ok<T>(const EsParams<T>&); \
-    template int scatter_two_planes<T>(const EsParams<T>&, \
-            const BucketScratch&, uint32_t, T*, int, T*, hipStream_t, bool); \
+    template int planes_per_pass<T>(const EsParams<T>&); \
+    template int scatter_planes<T>(const EsParams<T>&, \
+            const BucketScratch&, uint32_t, T* const*, int, hipStream_t, \
+            bool); \
     template int gather<T>(const EsParams<T>&, const BucketScratch&, \
             uint32_t, const T*, T*, hipStream_t); \
     template int screen_corr_2d<T>(const ImageParams<T>&, const T*, T*, \

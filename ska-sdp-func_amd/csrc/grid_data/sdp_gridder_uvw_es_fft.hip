@@ -51,7 +51,7 @@ struct sdp_GridderUvwEsFft
 
     // Device state.
     void* grid;                 // G x G complex plane
-    void* grid2;                // second plane (3-D two-plane tile passes)
+    void* grid_x[2];            // further planes of a 3-D multi-plane pass
     void* tables;               // conv_corr | quad kernel | nodes | weights
     int ntiles;
     int ncoarse;
@@ -508,40 +508,44 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
                     weight, grid, status);
         }
         else if (plane + 1 < nplanes &&
-                sdp_es::two_plane_scatter_ok(es_params<T>(plan, plane)))
+                sdp_es::planes_per_pass(es_params<T>(plan, plane)) > 1)
         {
-            // 3-D: this plane and the next in one tile-kernel pass (the
-            // entries' staging is shared), the next one into grid2.
-            if (!plan->grid2)
+            // 3-D: this plane and the next one or two in one tile-kernel
+            // pass (the entries' staging is shared), the others into
+            // plan-owned grids; then each plane's FFT and image step.
+            const int np = std::min(nplanes - plane,
+                    sdp_es::planes_per_pass(es_params<T>(plan, plane)));
+            T* grids[3] = {grid, nullptr, nullptr};
+            const size_t cells = (size_t)plan->grid_size * plan->grid_size;
+            for (int q = 1; q < np; ++q)
             {
-                const size_t cells = (size_t)plan->grid_size *
-                        plan->grid_size;
-                SDP_HIP_CHECK(hipMalloc(&plan->grid2, cells * 2 * sizeof(T)),
+                if (!plan->grid_x[q - 1])
+                {
+                    SDP_HIP_CHECK(hipMalloc(&plan->grid_x[q - 1],
+                            cells * 2 * sizeof(T)), status);
+                    if (*status) return;
+                }
+                grids[q] = (T*)plan->grid_x[q - 1];
+            }
+            timing_mark(plan, 1);
+            int e = sdp_es::scatter_planes<T>(es_params<T>(plan, plane),
+                    plan->scratch, n_items, grids, np, plan->stream, sparse);
+            if (e) { *status = (sdp_Error)e; return; }
+            for (int q = 0; q < np; ++q, ++plane)
+            {
+                timing_mark(plan, 2);
+                grid_to_image<T>(plan, ip, plane, grids[q], dirty, sparse,
                         status);
                 if (*status) return;
+                if (plane == nplanes - 1)
+                {
+                    e = sdp_es::apply_correction<T>(ip, dirty, plan->stream);
+                    if (e) { *status = (sdp_Error)e; return; }
+                }
+                timing_mark(plan, 4);
+                timing_collect_range(plan, q == 0 ? 1 : 2, 4, kGridSlots);
             }
-            T* grid2 = (T*)plan->grid2;
-            timing_mark(plan, 1);
-            int e = sdp_es::scatter_two_planes<T>(es_params<T>(plan, plane),
-                    plan->scratch, n_items, grid, plane + 1, grid2,
-                    plan->stream, sparse);
-            if (e) { *status = (sdp_Error)e; return; }
-            timing_mark(plan, 2);
-            grid_to_image<T>(plan, ip, plane, grid, dirty, sparse, status);
-            if (*status) return;
-            timing_mark(plan, 4);
-            timing_collect_range(plan, 1, 4, kGridSlots);
-            ++plane;
-            timing_mark(plan, 2);
-            grid_to_image<T>(plan, ip, plane, grid2, dirty, sparse, status);
-            if (*status) return;
-            if (plane == nplanes - 1)
-            {
-                e = sdp_es::apply_correction<T>(ip, dirty, plan->stream);
-                if (e) { *status = (sdp_Error)e; return; }
-            }
-            timing_mark(plan, 4);
-            timing_collect_range(plan, 2, 4, kGridSlots);
+            --plane;            // the loop's ++plane moves past the last
             continue;
         }
         else
@@ -671,7 +675,8 @@ void sdp_gridder_uvw_es_fft_free_plan(sdp_GridderUvwEsFft* plan)
 {
     if (!plan) return;
     if (plan->grid) (void)hipFree(plan->grid);
-    if (plan->grid2) (void)hipFree(plan->grid2);
+    for (void* g : plan->grid_x)
+        if (g) (void)hipFree(g);
     if (plan->tables) (void)hipFree(plan->tables);
     sdp_es::BucketScratch& s = plan->scratch;
     if (s.table) (void)hipFree(s.table);
