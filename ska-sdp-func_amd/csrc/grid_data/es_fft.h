@@ -65,11 +65,6 @@ void fft_twiddles_destroy(FftTwiddles* tw);
 int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
         float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream);
 // Gridding, part 2: last column pass + screen/correction into dirty.
-// 3-D: planes plane (grid) and plane + 1 (grid2), each after its
-// fft_grid_rows_cols, added to dirty in one column pass (f32, fused FFT).
-int fft_grid_to_image_pair(const ImageParams<float>& ip, int plane,
-        const FftTwiddles& tw, float* grid, float* grid2, float* dirty,
-        hipStream_t stream);
 int fft_grid_to_image(const ImageParams<float>& ip, int plane,
         const FftTwiddles& tw, float* grid, float* dirty, hipStream_t stream);
 

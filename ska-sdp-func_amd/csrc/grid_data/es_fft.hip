@@ -645,19 +645,13 @@ k_cols_a_grid(float2* __restrict__ grid, int M, const float2* __restrict__ W)
 // k - k0. 2-D: dirty = (dirty + checker * Re) / correction
 // (conv_corr_and_scaling, sdp_gridder_uvw_es_fft.cpp:706-740); 3-D:
 // dirty += checker * Re(F * phasor(w)) (apply_w_screen_and_sum, :664-700).
-// PAIR (3-D): grid2 holds w-plane plane + 1 after the same row and column-A
-// passes; its column transform runs after the first one's in the same
-// workgroup and both planes are added to the image in one read-modify-write
-// (same rounding as two passes: (dirty + plane) + plane + 1).
-template<int N1, int N2, bool DO_W, bool PAIR = false>
+template<int N1, int N2, bool DO_W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_COLB_WAVES)))
 k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
         ImageParams<float> ip, int plane, int k0, int M,
-        const float2* __restrict__ W,
-        const float2* __restrict__ grid2 = nullptr)
+        const float2* __restrict__ W)
 {
 #pragma clang fp contract(off)
-    static_assert(!PAIR || DO_W, "plane pairs: 3-D");
     constexpr int G = N1 * N2, B = ColPlan<N1>::B;
     using F = ColFft<N1, 1>;
     extern __shared__ float2 lds[];
@@ -665,7 +659,6 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
     const int k2 = blockIdx.x;
     const int h = M / 2;
     const Buf gb(grid, grid_bytes(G, 0));
-    const Buf gb2(PAIR ? grid2 : grid, grid_bytes(G, 0));
     const BufF db(dirty, (uint32_t)((size_t)ip.N * ip.N * 4));
     F f;
     f.init(p, W, G);
@@ -696,19 +689,19 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
         }
         f.transform(v, pq, lds, ColIdx<B>{cq});
         const float ccx = ip.conv_corr[min(abs(col - h), h)];
-        // This plane's contribution to output element (e, i).
-        auto contrib = [&](int e, float2 x, int pl) -> float {
+        F::store_output(v, [&](int e, int i, float2 x) {
             const int iy = k2 + N2 * (pq + e) - k0;
             const bool in = ok && (unsigned)iy < (unsigned)M;
             const int ix = col;
             const int xo = ix - h, yo = iy - h;
+            const uint32_t off = ((uint32_t)iy * ip.N + ix) * 4u;
             float val;
             if constexpr (DO_W)
             {
                 // Only the image rows need the w-screen (a third of the
                 // padded rows are cropped; rows are wave-uniform).
                 float re = 0.0f, im = 0.0f;
-                if (in) phasor(ip, pl, abs(xo), abs(yo), -1.0f, re, im);
+                if (in) phasor(ip, plane, abs(xo), abs(yo), -1.0f, re, im);
                 val = x.x * re - x.y * im;
             }
             else
@@ -716,27 +709,7 @@ k_cols_b_grid(const float2* __restrict__ grid, float* __restrict__ dirty,
                 val = x.x;
             }
             if ((ix + iy) & 1) val = -val;
-            return val;
-        };
-        if constexpr (PAIR)
-        {
-            F::store_output(v, [&](int e, int i, float2 x) {
-                prev[i] = prev[i] + contrib(e, x, plane);
-            });
-            F::load_input(v, [&](int e) {
-                return ok ? gb2.load(vo, so + e * (uint32_t)G * 8u)
-                          : make_float2(0.f, 0.f);
-            });
-            __syncthreads();       // the first transform's LDS reads done
-            f.transform(v, pq, lds, ColIdx<B>{cq});
-        }
-        F::store_output(v, [&](int e, int i, float2 x) {
-            const int iy = k2 + N2 * (pq + e) - k0;
-            const bool in = ok && (unsigned)iy < (unsigned)M;
-            const int ix = col;
-            const int yo = iy - h;
-            const uint32_t off = ((uint32_t)iy * ip.N + ix) * 4u;
-            float out = prev[i] + contrib(e, x, PAIR ? plane + 1 : plane);
+            float out = prev[i] + val;
             if constexpr (!DO_W)
             {
                 // inv_correction (es_image_dev.h), 2-D branch, same order.
@@ -1619,22 +1592,6 @@ int grid_to_image(const Geometry& g, const ImageParams<float>& ip, int plane,
     return st;
 }
 
-// 3-D: planes plane (grid) and plane + 1 (grid2), both after their row and
-// column-A passes, into the image in one column-B pass.
-template<int N1, int N2>
-int grid_to_image_pair(const Geometry& g, const ImageParams<float>& ip,
-        int plane, const float2* W, const float2* grid, const float2* grid2,
-        float* dirty, hipStream_t stream)
-{
-    sdp_Error st = SDP_SUCCESS;
-    const dim3 blocks = col_grid<k_cols_b_grid<N1, N2, true, true>>(N2, g.M,
-            ColPlan<N1>::B, 256, kColLdsBytes, kPairRounds);
-    k_cols_b_grid<N1, N2, true, true><<<blocks, 256, kColLdsBytes, stream>>>(
-            grid, dirty, ip, plane, g.k0, g.M, W, grid2);
-    SDP_HIP_CHECK_LAUNCH(&st);
-    return st;
-}
-
 // Real-output (Hermitian) form of the 2-D gridding transform, for grids of
 // 2048 to 8192 (at 16384 the row pass's rows do not fit the registers; the
 // complex form serves 1024 and 16384, and every 3-D plane).
@@ -1936,17 +1893,6 @@ int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
                 (float2*)grid, tiles, ncoarse, (uint32_t*)tw.masks, stream)))
     SDP_ES_FFT_DISPATCH(g.G, (grid_rows_cols<N1, N2>(g, W, (float2*)grid,
             tiles, ncoarse, stream)))
-}
-
-int fft_grid_to_image_pair(const ImageParams<float>& ip, int plane,
-        const FftTwiddles& tw, float* grid, float* grid2, float* dirty,
-        hipStream_t stream)
-{
-    if (!ip.do_w) return SDP_ERR_RUNTIME;
-    const Geometry g = geometry(ip);
-    const float2* W = (const float2*)tw.table;
-    SDP_ES_FFT_DISPATCH(g.G, (grid_to_image_pair<N1, N2>(g, ip, plane, W,
-            (const float2*)grid, (const float2*)grid2, dirty, stream)))
 }
 
 int fft_grid_to_image(const ImageParams<float>& ip, int plane,

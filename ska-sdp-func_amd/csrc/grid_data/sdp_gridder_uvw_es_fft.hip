@@ -531,35 +531,6 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
             int e = sdp_es::scatter_planes<T>(es_params<T>(plan, plane),
                     plan->scratch, n_items, grids, np, plan->stream, sparse);
             if (e) { *status = (sdp_Error)e; return; }
-            if constexpr (std::is_same<T, float>::value)
-            {
-                if (np == 2 && plan->fused_fft)
-                {
-                    // Both planes' row and column-A passes, then one
-                    // column-B pass adds both to the image.
-                    timing_mark(plan, 2);
-                    for (int q = 0; q < 2 && !e; ++q)
-                        e = sdp_es::fft_grid_rows_cols(ip, plan->fft_tw,
-                                grids[q], sparse ? plan->scratch.bin_count :
-                                nullptr, plan->ncoarse, plan->stream);
-                    if (e) { *status = (sdp_Error)e; return; }
-                    timing_mark(plan, 3);
-                    e = sdp_es::fft_grid_to_image_pair(ip, plane,
-                            plan->fft_tw, grids[0], grids[1], dirty,
-                            plan->stream);
-                    if (e) { *status = (sdp_Error)e; return; }
-                    plane += 1;
-                    if (plane == nplanes - 1)
-                    {
-                        e = sdp_es::apply_correction<T>(ip, dirty,
-                                plan->stream);
-                        if (e) { *status = (sdp_Error)e; return; }
-                    }
-                    timing_mark(plan, 4);
-                    timing_collect_range(plan, 1, 4, kGridSlots);
-                    continue;
-                }
-            }
             for (int q = 0; q < np; ++q, ++plane)
             {
                 timing_mark(plan, 2);
