@@ -575,6 +575,40 @@ __device__ __forceinline__ bool z_exceeds(const ZTest& zt, double val)
     return z > zt.thr || z < -zt.thr;
 }
 
+// z_exceeds for the EPL register slots of a lane at once, as bit j of the
+// result. The reciprocal test runs branch-free on every slot; only when some
+// lane's slot falls inside the exact-division band (or the test has no fast
+// form) does the whole wave redo the slots with z_exceeds, which gives the
+// same bits (outside the band the two agree). Per-slot divergent branches
+// cost ~40 scalar / exec-mask instructions each.
+template<int EPL, class Val>
+__device__ __forceinline__ uint32_t z_bits(const ZTest& zt, const Val& val)
+{
+#pragma clang fp contract(off)
+    uint32_t bits = 0;
+    bool exact = zt.dev0 || !zt.fast;
+    if (!exact)
+    {
+        bool unsure = false;
+#pragma unroll
+        for (int j = 0; j < EPL; ++j)
+        {
+            const double aq = fabs(0.6795 * (val(j) - zt.med) * zt.inv);
+            bits |= (aq > zt.thr ? 1u : 0u) << j;
+            unsure = unsure || fabs(aq - zt.thr) <= zt.band;
+        }
+        exact = __builtin_amdgcn_ballot_w64(unsure) != 0;
+    }
+    if (exact)
+    {
+        bits = 0;
+#pragma unroll
+        for (int j = 0; j < EPL; ++j)
+            bits |= (z_exceeds(zt, val(j)) ? 1u : 0u) << j;
+    }
+    return bits;
+}
+
 // Window spread (:224-240, :316-337): channel d is flagged if it triggered,
 // or a trigger sits i <= window channels above it and d > 0, or i <= window
 // channels below it.
@@ -631,11 +665,13 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
     const int k_s = mid_index(prm.ns);
 
     bool ch_ok[EPL], smp_ok[EPL];
+    uint32_t ok_bits = 0;          // bit j: ch_ok[j]
 #pragma unroll
     for (int j = 0; j < EPL; ++j)
     {
         const int c = lane0 + 64 * j;
         ch_ok[j] = FULL || c < C;
+        ok_bits |= (ch_ok[j] ? 1u : 0u) << j;
         smp_ok[j] = FULL || (c < C && (c % prm.step) == 0 &&
                 (c / prm.step) < prm.ns);
     }
@@ -756,18 +792,23 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
             situation = zmed > prm.thr_bb || zmed < -prm.thr_bb;
         }
 
-        // Magnitude triggers (:214-241) into trig_all.
+        // Magnitude triggers (:214-241) into trig_all, or straight to the
+        // flags (the stores only where some lane triggered).
         {
-            const ZTest zt = make_ztest(median, mediandev, prm.thr_mag);
-#pragma unroll
-            for (int j = 0; j < EPL; ++j)
+            const uint32_t mag_bits = situation ? ok_bits :
+                    z_bits<EPL>(make_ztest(median, mediandev, prm.thr_mag),
+                            [&](int j) { return (double)m[j]; }) & ok_bits;
+            if (prm.window > 0)
             {
-                const bool tr = ch_ok[j] &&
-                        (situation || z_exceeds(zt, (double)m[j]));
-                const int c = lane + 64 * j;
-                if (prm.window > 0 && ch_ok[j]) trig_all[c] = tr ? 1 : 0;
-                if (prm.window == 0 && tr)
-                    set_flag(frow, j, P, lane);
+#pragma unroll
+                for (int j = 0; j < EPL; ++j)
+                    if (ch_ok[j]) trig_all[lane + 64 * j] = (mag_bits >> j) & 1u;
+            }
+            else if (__builtin_amdgcn_ballot_w64(mag_bits != 0))
+            {
+#pragma unroll
+                for (int j = 0; j < EPL; ++j)
+                    if ((mag_bits >> j) & 1u) set_flag(frow, j, P, lane);
             }
         }
 
@@ -794,24 +835,30 @@ __global__ __launch_bounds__(64 * kWaves) FLAGGER_WAVES void k_flagger(
                 mediandevvar = select_tracked<double, EPL, kCandRegs>(kv,
                         k_s, prm.ns, tk_vdev, (uint64_t*)cand, lane, 5);
             }
-            const ZTest zv = make_ztest(medianvar, mediandevvar, prm.thr_var);
-#pragma unroll
-            for (int j = 0; j < EPL; ++j)
+            const uint32_t var_bits = z_bits<EPL>(
+                    make_ztest(medianvar, mediandevvar, prm.thr_var),
+                    [&](int j) { return fabs(transit[j]); }) & ok_bits;
+            if (prm.window > 0)
             {
-                const bool tv = ch_ok[j] && z_exceeds(zv, fabs(transit[j]));
-                const int c = lane + 64 * j;
-                if (prm.window > 0)
+#pragma unroll
+                for (int j = 0; j < EPL; ++j)
                 {
-                    if (ch_ok[j])
-                    {
-                        trig_var[c] = tv ? 1 : 0;
-                        if (tv) trig_all[c] = 1;
-                    }
+                    const int c = lane + 64 * j;
+                    const uint32_t tv = (var_bits >> j) & 1u;
+                    if (ch_ok[j]) trig_var[c] = tv;
+                    if (tv) trig_all[c] = 1;
                 }
-                else if (tv)
+            }
+            else if (__builtin_amdgcn_ballot_w64(var_bits != 0))
+            {
+#pragma unroll
+                for (int j = 0; j < EPL; ++j)
                 {
-                    set_flag(frow, j, P, lane);
-                    set_flag(fprev, j, P, lane);
+                    if ((var_bits >> j) & 1u)
+                    {
+                        set_flag(frow, j, P, lane);
+                        set_flag(fprev, j, P, lane);
+                    }
                 }
             }
         }
