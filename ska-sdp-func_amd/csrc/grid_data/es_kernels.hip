@@ -1883,6 +1883,39 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     }
     auto write_tile = [&](float* __restrict__ g, const f32x4 (&ar)[4],
             const f32x4 (&ai)[4]) {
+        // A tile owned whole by this work item and inside the grid (every
+        // tile when G is a multiple of 64): straight-line stores, no
+        // per-element bounds or mode branches.
+        if (npieces == 1 && r0 + 64 <= p.G && c0 + 64 <= p.G)
+        {
+            float* base = g + ((size_t)(r0 + sub_r + kq * 4) * p.G + c0 + i) * 2;
+            if (accumulate)
+            {
+#pragma unroll
+                for (int cblk = 0; cblk < 4; ++cblk)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+                    {
+                        float* dst = base + ((size_t)rr * p.G + cblk * 16) * 2;
+                        float2 v = *(const float2*)dst;
+                        v.x += ar[cblk][rr];
+                        v.y += ai[cblk][rr];
+                        *(float2*)dst = v;
+                    }
+            }
+            else
+            {
+#pragma unroll
+                for (int cblk = 0; cblk < 4; ++cblk)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr)
+                    {
+                        float* dst = base + ((size_t)rr * p.G + cblk * 16) * 2;
+                        *(float2*)dst = make_float2(ar[cblk][rr], ai[cblk][rr]);
+                    }
+            }
+            return;
+        }
 #pragma unroll
         for (int cblk = 0; cblk < 4; ++cblk)
         {
