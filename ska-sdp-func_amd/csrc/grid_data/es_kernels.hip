@@ -297,7 +297,7 @@ __global__ __launch_bounds__(NT) void k_bucket_count(EsParams<T> p,
         const T* __restrict__ uvw, const T* __restrict__ freq,
         uint32_t* __restrict__ stable, uint32_t* __restrict__ gtable)
 {
-    __shared__ uint32_t hist[kBinsPerPass];
+    __shared__ uint32_t hist[kBinsPerPass + NT];
     __shared__ uint32_t shist[kCountChunks][kMaxSuperBins];
     const int pass_base = blockIdx.y * kBinsPerPass;
     const int nb = min(kBinsPerPass, p.nbins - pass_base);
@@ -326,17 +326,27 @@ __global__ __launch_bounds__(NT) void k_bucket_count(EsParams<T> p,
                 int tu0, tu1, tv0, tv1;
                 tile_span<T, MODE>(p, f.u0, f.u1, f.v0, f.v1, tu0, tu1, tv0,
                         tv1);
-                for (int tu = tu0; tu <= tu1; ++tu)
-                    for (int tv = tv0; tv <= tv1; ++tv)
+                // A support spans at most 2 tiles / super bins per axis;
+                // counts outside the span go to this thread's dummy word.
+                const int su0 = tu0 >> p.sshift, sv0 = tv0 >> p.sshift;
+                const int su1 = tu1 >> p.sshift, sv1 = tv1 >> p.sshift;
+                uint32_t* dmy = &hist[kBinsPerPass + threadIdx.x];
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+#pragma unroll
+                    for (int c2 = 0; c2 < 2; ++c2)
                     {
-                        const int b = fine_bin(p, tu, tv) - pass_base;
-                        if (b >= 0 && b < nb) atomicAdd(&hist[b], 1u);
+                        const int b = fine_bin(p, tu0 + a, tv0 + c2) - pass_base;
+                        const bool ok = tu0 + a <= tu1 && tv0 + c2 <= tv1 &&
+                                b >= 0 && b < nb;
+                        atomicAdd(ok ? &hist[b] : dmy, 1u);
+                        if (supers)
+                        {
+                            const bool oks = su0 + a <= su1 && sv0 + c2 <= sv1;
+                            atomicAdd(oks ? &sh[(su0 + a) * p.nsuper + sv0 + c2] :
+                                    dmy, 1u);
+                        }
                     }
-                if (supers)
-                    for (int su = tu0 >> p.sshift; su <= tu1 >> p.sshift; ++su)
-                        for (int sv = tv0 >> p.sshift; sv <= tv1 >> p.sshift;
-                                ++sv)
-                            atomicAdd(&sh[su * p.nsuper + sv], 1u);
             }
         }
     }
