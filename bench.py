@@ -52,6 +52,28 @@ HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3        # MI355X_MICROARCH.md: FP32 vector = f32 MFMA
 
 
+def csrc_sha16(root=ROOT):
+    """sha256 (16 hex digits) of the native sources the library is built
+    from: ska-sdp-func_amd/csrc/**, include/** and the Makefile (paths and
+    contents, sorted). profiles/pmc_traffic.json records the value of the
+    build its counters were taken on; bench.py reports that traffic only
+    when the current sources hash to the same value."""
+    import hashlib
+    h = hashlib.sha256()
+    files = []
+    for sub in ("ska-sdp-func_amd/csrc", "include"):
+        for dp, _, fns in os.walk(os.path.join(root, sub)):
+            files += [os.path.join(dp, f) for f in fns]
+    files.append(os.path.join(root, "ska-sdp-func_amd", "Makefile"))
+    for f in sorted(files):
+        if "__pycache__" in f or not os.path.isfile(f):
+            continue
+        h.update(os.path.relpath(f, root).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -168,6 +190,32 @@ def host_cpus():
             "usable": usable}
 
 
+def h2d_time(torch, dev, tensors, reps=3):
+    """Host -> device copy of a call's inputs (reported beside
+    the Mvis/s, never part of it): the device tensors are staged once into
+    pinned host buffers, then copied back to HBM reps times on the current
+    stream (non-blocking, one synchronisation per rep). Returns the mean ms
+    per copy of all tensors and the bytes moved."""
+    host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            for t in tensors]
+    for h, t in zip(host, tensors):
+        h.copy_(t)
+    nbytes = sum(t.numel() * t.element_size() for t in tensors)
+    torch.cuda.synchronize(dev)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for h, t in zip(host, tensors):
+            t.copy_(h, non_blocking=True)
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t0)
+    del host
+    ms = 1e3 * sum(times) / len(times)
+    return {"h2d_ms": round(ms, 3), "bytes": nbytes,
+            "GBs": round(nbytes / (ms * 1e-3) / 1e9, 1),
+            "what": "uvw + vis + weight from pinned host memory"}
+
+
 def cpu_baseline(args, G, support, beta, uv_scale):
     """Oracle ('port') CPU gridder timed on the host cores.
 
@@ -271,6 +319,10 @@ def run_config3(args, torch, dev, dist, world, rank):
     G = plan.grid_size
     grid_buf = (torch.empty((G, G), dtype=torch.complex64, device=dev)
                 if world > 1 else None)
+    # Mode "grid" reduces the row spectra of the Hermitian part (fused f32
+    # plans) instead of the whole grid: what travels per rank.
+    spec = plan.row_spectra()
+    grid_red_bytes = (spec[0] * spec[2] * 8 if spec else G * G * 8)
 
     def sync():
         torch.cuda.synchronize(dev)
@@ -322,14 +374,18 @@ def run_config3(args, torch, dev, dist, world, rank):
             modes[mode] = {
                 "mvis_s": round(total * args.c3_steps / t / 1e6, 3),
                 "ms_per_step": round(1e3 * t / args.c3_steps, 3),
-                "reduce": ("RCCL reduce of the per-GPU 8192^2 complex64 "
-                           "grids (512 MiB) before one FFT on rank 0"
+                "reduce": (f"per-GPU row pass of the inverse FFT, then "
+                           f"one RCCL reduce of the row spectra "
+                           f"({grid_red_bytes / 1e6:.0f} MB; the whole "
+                           f"{G}^2 grid is {G * G * 8 / 2**20:.0f} MiB) "
+                           f"before the column passes on rank 0"
                            if mode == "grid" else
                            "RCCL reduce of the per-GPU partial images "
                            f"({args.image}^2 f32, "
                            f"{args.image ** 2 * 4 / 1e6:.0f} MB)"),
-                "reduce_ms": reduce_ms(grid_buf if mode == "grid"
-                                       else dirty),
+                "reduce_ms": reduce_ms(
+                    torch.empty(grid_red_bytes // 8, dtype=torch.complex64,
+                                device=dev) if mode == "grid" else dirty),
             }
     # Per-phase device times of one whole call on this rank's shard (HIP
     # events on the plan stream, summed over the call's row batches),
@@ -367,11 +423,17 @@ def run_config3(args, torch, dev, dist, world, rank):
         t_sc = phases["bucket"] + phases["tile_kernel"]
         t_fi = phases["fft"] + phases["image"]
         pred = {"n_gpus": 8,
-                "modes": predicted_speedup(t_sc, t_fi, 8, G * G * 8,
-                                           args.image ** 2 * 4),
+                "modes": predicted_speedup(t_sc, t_fi, 8, grid_red_bytes,
+                                           args.image ** 2 * 4,
+                                           grid_packed=spec is not None),
+                "grid_mode": ("per-rank row pass, reduce of the (G/2 + 1) x "
+                              "M Hermitian row spectra, column passes on "
+                              "the destination" if spec else
+                              "reduce of the whole grid"),
                 "inputs": {"scatter_ms": round(t_sc, 3),
                            "fft_image_ms": round(t_fi, 3)}}
     best = max(modes, key=lambda k: modes[k]["mvis_s"])
+    h2d = h2d_time(torch, dev, [uvw, vis, weight])
     out = {
         "workload": (f"ES-FFT gridding, {args.c3_rows} rows x "
                      f"{args.c3_chan} chan in total (1.0-1.49 GHz), image "
@@ -385,6 +447,12 @@ def run_config3(args, torch, dev, dist, world, rank):
         "phases_ms": phases,
         "roofline": roofline,
         "predicted_8gpu": pred,
+        # This rank's inputs over PCIe (per GPU; not in mvis_s).
+        "h2d_ms": h2d["h2d_ms"],
+        "h2d": h2d,
+        "pcie_inclusive_mvis_s": round(
+            total / ((modes[best]["ms_per_step"] + h2d["h2d_ms"]) * 1e-3)
+            / 1e6, 3),
         "steps": args.c3_steps,
         "scaling": "strong",
     }
@@ -684,6 +752,10 @@ def main():
             "phases_ms": {k: round(v / phase_steps, 4) for k, v in dph.items()},
         }
 
+    # Host -> device transfer of the config-2 inputs, reported beside the
+    # HBM-resident rate.
+    h2d = h2d_time(torch, dev, [uvw, vis, weight])
+
     # Roofline of the dominant kernel of a gridding call.
     kern_bytes = {
         "tile_kernel": scatter_bytes(args.rows, args.chan, G),
@@ -702,16 +774,22 @@ def main():
                     "image": ("k_cols_b_grid (last FFT pass + screen)"
                               if plan.fused_fft else "k_screen_corr_2d")}
     traffic = None
+    traffic_src = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            # Counters were collected at one workload: only reported for it.
+            # Counters were collected at one workload on one build: only
+            # reported for that workload and sources hashing to that build.
             wl = pmc.get("_workload", {})
+            traffic_src = {"file": "profiles/pmc_traffic.json",
+                           "csrc_sha16": pmc.get("_csrc_sha16"),
+                           "current_csrc_sha16": csrc_sha16()}
             if (wl.get("rows") == args.rows and wl.get("chan") == args.chan
                     and wl.get("image") == args.image
-                    and wl.get("eps") == args.eps):
+                    and wl.get("eps") == args.eps
+                    and pmc.get("_csrc_sha16") == csrc_sha16()):
                 traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
@@ -807,6 +885,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 # Counter-based view of the same launch: PMC HBM bytes over
                 # the event time (the scatter skips empty tiles, so its
                 # algorithmic count includes grid bytes it never writes).
@@ -836,6 +915,13 @@ def main():
                               / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             },
             "degrid": degrid,
+            # Inputs resident in HBM when the clock starts; the PCIe copy of
+            # one GPU's inputs from pinned host memory is timed separately.
+            "h2d_ms": h2d["h2d_ms"],
+            "h2d": h2d,
+            "pcie_inclusive_mvis_s": round(
+                args.rows * args.chan / ((ms_per_step + h2d["h2d_ms"])
+                                         * 1e-3) / 1e6, 3),
             "grid_reduce_mode": grid_reduce,
             "config3": config3,
             "wstack_3d": wstack,

@@ -137,10 +137,13 @@ void sdp_grid_wstack_wtower_degrid_planes(
  * w-stack planes, for load-balanced sharding across GPUs. Plane iw is the
  * reference's w-stack plane index (w f / c in [iw d - d/2, (iw + 1) d -
  * d/2), d = w_tower_height * w_step, sdp_grid_wstack_wtower.cpp:336-343);
- * it is processed iff plane_first <= iw < plane_first + n and
- * plane_mask[iw - plane_first] != 0, plane_mask a 1-D int32 array of n
- * entries (host or device). Disjoint masks covering every plane give images
- * / visibilities that sum to the grid_all / degrid_all ones. */
+ * it is processed iff plane_mask[clamp(iw - plane_first, 0, n - 1)] != 0,
+ * plane_mask a 1-D int32 array of n entries (host or device): planes below
+ * plane_first belong to the owner of entry 0, planes past the range to the
+ * owner of entry n - 1. Disjoint masks covering the n entries therefore
+ * cover every plane, and give images / visibilities that sum to the
+ * grid_all / degrid_all ones even where the caller's plane-range model
+ * misses a plane. */
 void sdp_grid_wstack_wtower_grid_plane_set(
         const sdp_Mem* vis,
         double freq0_hz,

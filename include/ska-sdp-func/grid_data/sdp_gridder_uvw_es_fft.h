@@ -138,6 +138,36 @@ void sdp_grid_uvw_es_fft_finish(
         sdp_Error* status
 );
 
+/* MI355X extension: finish in two halves around a reduction of row
+ * spectra (multi-GPU "grid" mode; the split of the reference's inverse
+ * FFT, sdp_gridder_uvw_es_fft.cpp:660-701).
+ * _rows runs the first pass of the inverse FFT (the row FFTs, real-output
+ * form where the plan uses it) in place on a scattered grid; the data the
+ * remaining passes read is then grid rows [0, rows) x columns [col0, col0
+ * + ncols), reported by _row_spectra (returns 0 for plans without the
+ * fused f32 FFT: f64 or non-power-of-two grids). Both halves are linear,
+ * so per-GPU grids can be summed over that block alone (178 MB at G 8192,
+ * N 5440, against 512 MiB for the whole grid). _finish_rows runs the
+ * remaining column passes + screen + correction into dirty_image.
+ * scatter + rows + finish_rows == scatter + finish. */
+int sdp_gridder_uvw_es_fft_row_spectra(
+        const sdp_GridderUvwEsFft* plan,
+        int64_t* rows,
+        int64_t* col0,
+        int64_t* ncols
+);
+void sdp_grid_uvw_es_fft_rows(
+        sdp_GridderUvwEsFft* plan,
+        sdp_Mem* grid,
+        sdp_Error* status
+);
+void sdp_grid_uvw_es_fft_finish_rows(
+        sdp_GridderUvwEsFft* plan,
+        sdp_Mem* grid,
+        sdp_Mem* dirty_image,
+        sdp_Error* status
+);
+
 #ifdef __cplusplus
 }
 #endif

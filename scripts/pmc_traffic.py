@@ -74,7 +74,13 @@ def main():
         res[ph]["write_kib"] += w
         res[ph]["kernels"][short] = {"fetch_kib": f, "write_kib": w,
                                      "dispatches_per_call": len(fetch.get(name, [])) / calls}
+    sys.path.insert(0, os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))))
+    from bench import csrc_sha16
     out = {"_calls": calls,
+           # The build the counters describe: bench.py reports the traffic
+           # only while the sources hash to this value.
+           "_csrc_sha16": csrc_sha16(),
            # bench.py reports the traffic only for this workload (the bench
            # arguments the counters were collected with; defaults here).
            "_workload": {"rows": 10000000, "chan": 1, "image": 5440,

@@ -453,21 +453,31 @@ void sdp_fft_2d_inplace_permuted(sdp_Mem* data, int is_forward,
                 "GPU array, side a power of two in [1024, 16384]");
         return;
     }
-    // Twiddle tables are built once per grid size and kept for the life of
-    // the process (at most five sizes, 1024..16384; a per-plane caller pays
-    // no allocation). The transform runs on the null stream, as the other
-    // sdp_fft_* kernels here, and returns when it is complete.
+    // Twiddle tables are built once per (device, grid size) and kept for the
+    // life of the process (at most five sizes, 1024..16384, per device; a
+    // per-plane caller pays no allocation). The tables live in the memory of
+    // the device current at creation, so the key carries the device: a call
+    // on another GPU with the same G gets its own tables. The transform runs
+    // on the null stream, as the other sdp_fft_* kernels here, and returns
+    // when it is complete.
     static std::mutex tw_lock;
-    static std::map<int, sdp_es::FftTwiddles> tw_cache;
+    static std::map<std::pair<int, int>, sdp_es::FftTwiddles> tw_cache;
     int e = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess)
+    {
+        *status = SDP_ERR_RUNTIME;
+        return;
+    }
     sdp_es::FftTwiddles tw;
     {
         std::lock_guard<std::mutex> guard(tw_lock);
-        auto it = tw_cache.find((int)G);
+        const auto key = std::make_pair(dev, (int)G);
+        auto it = tw_cache.find(key);
         if (it == tw_cache.end())
         {
             e = sdp_es::fft_twiddles_create((int)G, &tw);
-            if (!e) tw_cache.emplace((int)G, tw);
+            if (!e) tw_cache.emplace(key, tw);
         }
         else
         {

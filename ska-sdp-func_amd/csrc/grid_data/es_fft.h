@@ -64,6 +64,18 @@ void fft_twiddles_destroy(FftTwiddles* tw);
 // empty tiles: the row pass then reads nothing of those (they are zero).
 int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
         float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream);
+// The same in its two halves: the row pass alone, and column pass A of a
+// grid whose row pass is done. Both passes are linear in the grid, so the
+// row spectra of several grids (one per GPU) can be summed between them.
+int fft_grid_rows(const ImageParams<float>& ip, const FftTwiddles& tw,
+        float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream);
+int fft_grid_cols_a(const ImageParams<float>& ip, const FftTwiddles& tw,
+        float* grid, hipStream_t stream);
+// Where the row pass leaves the data the column passes read: grid rows
+// [0, rows), columns [col0, col0 + ncols) (real-output form: the G/2 + 1
+// rows of the Hermitian part; complex form: every row).
+void fft_grid_row_spectra(const ImageParams<float>& ip, int64_t* rows,
+        int64_t* col0, int64_t* ncols);
 // Gridding, part 2: last column pass + screen/correction into dirty.
 int fft_grid_to_image(const ImageParams<float>& ip, int plane,
         const FftTwiddles& tw, float* grid, float* dirty, hipStream_t stream);

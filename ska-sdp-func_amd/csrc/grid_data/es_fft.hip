@@ -1552,7 +1552,7 @@ Geometry geometry(const ImageParams<float>& ip)
 }
 
 template<int N1, int N2>
-int grid_rows_cols(const Geometry& g, const float2* W, float2* grid,
+int grid_rows(const Geometry& g, const float2* W, float2* grid,
         const uint32_t* tiles, int ncoarse, hipStream_t stream)
 {
     constexpr int G = N1 * N2;
@@ -1563,7 +1563,14 @@ int grid_rows_cols(const Geometry& g, const float2* W, float2* grid,
     k_rows_grid<G><<<row_blocks(G), RowPlan<G>::P, lds, stream>>>(
             grid, g.k0, g.M, W, tiles, ncoarse);
     SDP_HIP_CHECK_LAUNCH(&st);
-    if (st) return st;
+    return st;
+}
+
+template<int N1, int N2>
+int grid_cols_a(const Geometry& g, const float2* W, float2* grid,
+        hipStream_t stream)
+{
+    sdp_Error st = SDP_SUCCESS;
     k_cols_a_grid<N1, N2><<<col_grid<k_cols_a_grid<N1, N2>>(N1, g.M,
             ColPlan<N2>::B), 256,
             kColLdsBytes, stream>>>(grid, g.M, W);
@@ -1607,8 +1614,44 @@ bool herm_degrid_enabled(const ImageParams<float>& ip)
 }
 
 template<int N1, int N2>
-int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
+int grid_rows_herm(const Geometry& g, const float2* W, float2* grid,
         const uint32_t* tiles, int ncoarse, uint32_t* occ,
+        hipStream_t stream)
+{
+    constexpr int G = N1 * N2;
+    if constexpr (G < 2048 || G > 8192)
+    {
+        return SDP_ERR_INVALID_ARGUMENT;
+    }
+    else
+    {
+        sdp_Error st = SDP_SUCCESS;
+        if (tiles)
+        {
+            if (!occ) return SDP_ERR_RUNTIME;
+            static_assert(32 * occ_classes(G) <= 320, "one bit per thread");
+            k_row_occupancy<false><<<G / 64, 320, 0, stream>>>(tiles,
+                    ncoarse, G, occ);
+            SDP_HIP_CHECK_LAUNCH(&st);
+            if (st) return st;
+        }
+        // One H row per workgroup iteration; Z formed in column pass A
+        // (single-row form; the row-quad form measured 256 -> 242 us
+        // for the row + column pass at config 2 and was removed).
+        const size_t lds = row_lds_bytes(G);
+        SDP_HIP_CHECK((allow_lds<k_rows_herm1<G>>(lds)), &st);
+        if (st) return st;
+        const int blocks = std::min(G / 2 + 1, num_cus() *
+                (int)std::max<size_t>(1, (160 * 1024) / lds));
+        k_rows_herm1<G><<<blocks, RowPlan<G>::P, lds, stream>>>(
+                grid, g.k0, g.M, W, tiles ? occ : nullptr);
+        SDP_HIP_CHECK_LAUNCH(&st);
+        return st;
+    }
+}
+
+template<int N1, int N2>
+int grid_cols_a_herm(const Geometry& g, const float2* W, float2* grid,
         hipStream_t stream)
 {
     constexpr int G = N1 * N2;
@@ -1620,28 +1663,7 @@ int grid_rows_cols_herm(const Geometry& g, const float2* W, float2* grid,
     {
         using HS = HalfSplit<G / 2>;
         sdp_Error st = SDP_SUCCESS;
-        if (tiles)
         {
-            if (!occ) return SDP_ERR_RUNTIME;
-            static_assert(32 * occ_classes(G) <= 320, "one bit per thread");
-            k_row_occupancy<false><<<G / 64, 320, 0, stream>>>(tiles,
-                    ncoarse, G, occ);
-            SDP_HIP_CHECK_LAUNCH(&st);
-            if (st) return st;
-        }
-        {
-            // One H row per workgroup iteration; Z formed in column pass A
-            // (single-row form; the row-quad form measured 256 -> 242 us
-            // for the row + column pass at config 2 and was removed).
-            const size_t lds = row_lds_bytes(G);
-            SDP_HIP_CHECK((allow_lds<k_rows_herm1<G>>(lds)), &st);
-            if (st) return st;
-            const int blocks = std::min(G / 2 + 1, num_cus() *
-                    (int)std::max<size_t>(1, (160 * 1024) / lds));
-            k_rows_herm1<G><<<blocks, RowPlan<G>::P, lds, stream>>>(
-                    grid, g.k0, g.M, W, tiles ? occ : nullptr);
-            SDP_HIP_CHECK_LAUNCH(&st);
-            if (st) return st;
             constexpr int kTh = kPairsThreads;
             constexpr size_t kLds = kColLdsBytes * (kTh / 256);
             SDP_HIP_CHECK((allow_lds<k_cols_a_herm_pairs<HS::N1, HS::N2>>(
@@ -1883,16 +1905,46 @@ void fft_twiddles_destroy(FftTwiddles* tw)
     tw->G = 0;
 }
 
-int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
+int fft_grid_rows(const ImageParams<float>& ip, const FftTwiddles& tw,
         float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream)
 {
     const Geometry g = geometry(ip);
     const float2* W = (const float2*)tw.table;
     if (herm_enabled(ip))
-        SDP_ES_FFT_DISPATCH(g.G, (grid_rows_cols_herm<N1, N2>(g, W,
+        SDP_ES_FFT_DISPATCH(g.G, (grid_rows_herm<N1, N2>(g, W,
                 (float2*)grid, tiles, ncoarse, (uint32_t*)tw.masks, stream)))
-    SDP_ES_FFT_DISPATCH(g.G, (grid_rows_cols<N1, N2>(g, W, (float2*)grid,
+    SDP_ES_FFT_DISPATCH(g.G, (grid_rows<N1, N2>(g, W, (float2*)grid,
             tiles, ncoarse, stream)))
+}
+
+int fft_grid_cols_a(const ImageParams<float>& ip, const FftTwiddles& tw,
+        float* grid, hipStream_t stream)
+{
+    const Geometry g = geometry(ip);
+    const float2* W = (const float2*)tw.table;
+    if (herm_enabled(ip))
+        SDP_ES_FFT_DISPATCH(g.G, (grid_cols_a_herm<N1, N2>(g, W,
+                (float2*)grid, stream)))
+    SDP_ES_FFT_DISPATCH(g.G, (grid_cols_a<N1, N2>(g, W, (float2*)grid,
+            stream)))
+}
+
+int fft_grid_rows_cols(const ImageParams<float>& ip, const FftTwiddles& tw,
+        float* grid, const uint32_t* tiles, int ncoarse, hipStream_t stream)
+{
+    const int e = fft_grid_rows(ip, tw, grid, tiles, ncoarse, stream);
+    return e ? e : fft_grid_cols_a(ip, tw, grid, stream);
+}
+
+void fft_grid_row_spectra(const ImageParams<float>& ip, int64_t* rows,
+        int64_t* col0, int64_t* ncols)
+{
+    const Geometry g = geometry(ip);
+    // The row passes store a row's M centre outputs at columns [0, M)
+    // (k_rows_grid, k_rows_herm1: buffer base grid - k0).
+    *rows = herm_enabled(ip) ? g.G / 2 + 1 : g.G;
+    *col0 = 0;
+    *ncols = g.M;
 }
 
 int fft_grid_to_image(const ImageParams<float>& ip, int plane,

@@ -74,8 +74,11 @@ struct Geo
     int64_t P0, NP;                  // global w-layer index base and count
     int plane_offset, plane_stride;
     // Plane set (extension): when plane_mask is set, plane iw is processed
-    // iff mask_first <= iw < mask_first + mask_n and plane_mask[iw -
-    // mask_first] != 0 (offset / stride are then ignored). Device memory.
+    // iff plane_mask[clamp(iw - mask_first, 0, mask_n - 1)] != 0 (offset /
+    // stride are then ignored): a plane below or above the mask's range
+    // belongs to the owner of the first or last entry, so masks that
+    // partition the range partition every plane and no visibility is lost
+    // if the caller's range model misses one. Device memory.
     const int* plane_mask;
     int64_t mask_first, mask_n;
     int fused;                       // sort runs by (group, slot, layer)
@@ -87,8 +90,9 @@ __host__ __device__ __forceinline__ bool plane_selected(const Geo& g,
 {
     if (g.plane_mask)
     {
-        const int64_t m = iw - g.mask_first;
-        return m >= 0 && m < g.mask_n && g.plane_mask[m] != 0;
+        int64_t m = iw - g.mask_first;
+        m = m < 0 ? 0 : (m >= g.mask_n ? g.mask_n - 1 : m);
+        return g.mask_n > 0 && g.plane_mask[m] != 0;
     }
     return (iw - g.min_iw) % g.plane_stride == g.plane_offset;
 }

@@ -500,33 +500,45 @@ void run_grid(sdp_GridderUvwEsFft* plan, int64_t rows, int chan,
         timing_collect_range(plan, 0, 1, kGridSlots);
     }
     const int nplanes = plan->num_total_w_grids;
+    // Planes per 3-D tile-kernel pass: the extra planes' grids are allocated
+    // on first use (G^2 complex each: 2 GiB at G = 16384). An allocation
+    // that fails is not an error: the pass takes the planes that have a
+    // grid, down to the single-plane path the call ran before.
+    auto pass_planes = [&](int plane) -> int {
+        if (batched || plane + 1 >= nplanes) return 1;
+        int np = std::min(nplanes - plane,
+                sdp_es::planes_per_pass(es_params<T>(plan, plane)));
+        const size_t cells = (size_t)plan->grid_size * plan->grid_size;
+        for (int q = 1; q < np; ++q)
+        {
+            if (plan->grid_x[q - 1]) continue;
+            if (hipMalloc(&plan->grid_x[q - 1], cells * 2 * sizeof(T)) !=
+                    hipSuccess)
+            {
+                plan->grid_x[q - 1] = nullptr;
+                (void)hipGetLastError();   // clear the sticky error
+                SDP_LOG_WARNING("3-D gridding: no memory for a second "
+                        "w-plane grid; one plane per tile-kernel pass");
+                return q;
+            }
+        }
+        return np;
+    };
     for (int plane = 0; plane < nplanes && !*status; ++plane)
     {
+        const int np = pass_planes(plane);
         if (batched)
         {
             scatter_batches<T>(plan, plane, rows, rb, chan, uvw, freq, vis,
                     weight, grid, status);
         }
-        else if (plane + 1 < nplanes &&
-                sdp_es::planes_per_pass(es_params<T>(plan, plane)) > 1)
+        else if (np > 1)
         {
             // 3-D: this plane and the next one or two in one tile-kernel
             // pass (the entries' staging is shared), the others into
             // plan-owned grids; then each plane's FFT and image step.
-            const int np = std::min(nplanes - plane,
-                    sdp_es::planes_per_pass(es_params<T>(plan, plane)));
             T* grids[3] = {grid, nullptr, nullptr};
-            const size_t cells = (size_t)plan->grid_size * plan->grid_size;
-            for (int q = 1; q < np; ++q)
-            {
-                if (!plan->grid_x[q - 1])
-                {
-                    SDP_HIP_CHECK(hipMalloc(&plan->grid_x[q - 1],
-                            cells * 2 * sizeof(T)), status);
-                    if (*status) return;
-                }
-                grids[q] = (T*)plan->grid_x[q - 1];
-            }
+            for (int q = 1; q < np; ++q) grids[q] = (T*)plan->grid_x[q - 1];
             timing_mark(plan, 1);
             int e = sdp_es::scatter_planes<T>(es_params<T>(plan, plane),
                     plan->scratch, n_items, grids, np, plan->stream, sparse);
@@ -666,6 +678,34 @@ void timing_end(sdp_GridderUvwEsFft* plan, double wall_ms)
     plan->acc_ms[4] = wall_ms;
     plan->have_timing = 1;
 }
+
+// Grid (and image) arguments of the row-spectra halves: a fused-FFT 2-D
+// f32 plan and its G x G complex grid on the GPU.
+float* row_split_grid(sdp_GridderUvwEsFft* plan, sdp_Mem* grid,
+        sdp_Error* status)
+{
+    if (*status || !plan) return nullptr;
+    if (!sdp_gridder_uvw_es_fft_row_spectra(plan, nullptr, nullptr, nullptr))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("Row-spectra split needs a 2-D single-precision plan "
+                "with a power-of-two grid");
+        return nullptr;
+    }
+    const int64_t G = plan->grid_size;
+    if (sdp_mem_type(grid) != SDP_MEM_COMPLEX_FLOAT ||
+            sdp_mem_num_dims(grid) != 2 || sdp_mem_shape_dim(grid, 0) != G ||
+            sdp_mem_shape_dim(grid, 1) != G || !sdp_mem_is_c_contiguous(grid))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("grid must be a contiguous %lld x %lld complex float "
+                "array", (long long)G, (long long)G);
+        return nullptr;
+    }
+    void* p = sdp_mem_gpu_buffer(grid, status);
+    return *status ? nullptr : *(float**)p;
+}
+
 
 } // namespace
 
@@ -1097,6 +1137,55 @@ void sdp_grid_uvw_es_fft_finish(sdp_GridderUvwEsFft* plan, sdp_Mem* grid,
     else
         grid_to_image<float>(plan, image_params<float>(plan), 0,
                 *(float**)p_grid, *(float**)p_dirty, false, status);
+}
+
+int sdp_gridder_uvw_es_fft_row_spectra(const sdp_GridderUvwEsFft* plan,
+        int64_t* rows, int64_t* col0, int64_t* ncols)
+{
+    if (!plan || plan->is_double || !plan->fused_fft || plan->do_wstacking)
+        return 0;
+    int64_t r = 0, c = 0, n = 0;
+    sdp_es::fft_grid_row_spectra(image_params<float>(plan), &r, &c, &n);
+    if (rows) *rows = r;
+    if (col0) *col0 = c;
+    if (ncols) *ncols = n;
+    return 1;
+}
+
+
+void sdp_grid_uvw_es_fft_rows(sdp_GridderUvwEsFft* plan, sdp_Mem* grid,
+        sdp_Error* status)
+{
+    float* g = row_split_grid(plan, grid, status);
+    if (*status) return;
+    const int e = sdp_es::fft_grid_rows(image_params<float>(plan),
+            plan->fft_tw, g, nullptr, plan->ncoarse, plan->stream);
+    if (e) *status = (sdp_Error)e;
+}
+
+void sdp_grid_uvw_es_fft_finish_rows(sdp_GridderUvwEsFft* plan,
+        sdp_Mem* grid, sdp_Mem* dirty_image, sdp_Error* status)
+{
+    float* g = row_split_grid(plan, grid, status);
+    if (*status) return;
+    if (sdp_mem_type(dirty_image) != SDP_MEM_FLOAT ||
+            sdp_mem_num_dims(dirty_image) != 2 ||
+            sdp_mem_shape_dim(dirty_image, 0) != plan->image_size ||
+            sdp_mem_shape_dim(dirty_image, 1) != plan->image_size ||
+            !sdp_mem_is_c_contiguous(dirty_image))
+    {
+        *status = SDP_ERR_INVALID_ARGUMENT;
+        SDP_LOG_ERROR("dirty_image does not match the plan");
+        return;
+    }
+    void* p_dirty = sdp_mem_gpu_buffer(dirty_image, status);
+    if (*status) return;
+    const sdp_es::ImageParams<float> ip = image_params<float>(plan);
+    int e = sdp_es::fft_grid_cols_a(ip, plan->fft_tw, g, plan->stream);
+    if (!e)
+        e = sdp_es::fft_grid_to_image(ip, 0, plan->fft_tw, g,
+                *(float**)p_dirty, plan->stream);
+    if (e) *status = (sdp_Error)e;
 }
 
 } // extern "C"

@@ -275,11 +275,15 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
 // keeps the digit range that holds the k-th key: ~6 key bits per round,
 // ~30 instructions, against one compare + ballot + popcount probe per bit
 // of the bitwise search. Ends when the range holds a single key (read out)
-// or a single value (ties). bins: 64 words of LDS.
+// or a single value (ties). bins: 64 words of LDS. The caller guarantees
+// that [L, U) holds the k-th key; if a round finds no digit range past k
+// (the guarantee broken) ok is cleared and the caller falls back to the
+// search over every key, instead of reading lane 64 of a zero ballot.
 template<typename K, int N, class Keys>
 __device__ __forceinline__ K radix_select(const Keys& key, int k, K L, K U,
-        int n, uint32_t* bins, int lane, int& nround)
+        int n, uint32_t* bins, int lane, int& nround, bool& ok)
 {
+    ok = true;
     while (n > 1 && U - L > 1)
     {
         const K span = U - L;
@@ -300,6 +304,12 @@ __device__ __forceinline__ K radix_select(const Keys& key, int k, K L, K U,
         const uint32_t cnt = bins[lane];
         const uint32_t incl = wave_incl_scan(cnt);
         const uint64_t over = __builtin_amdgcn_ballot_w64(incl > (uint32_t)k);
+        if (over == 0)
+        {
+            ok = false;
+            wave_sync();
+            return L;
+        }
         const int b = (int)__builtin_ctzll(over);
         k -= (int)__builtin_amdgcn_readlane((int)(incl - cnt), b);
         n = __builtin_amdgcn_readlane((int)cnt, b);
@@ -441,6 +451,7 @@ __device__ __forceinline__ V select_tracked(const Keys& key, int k,
     }
     int nprobe = 0;
     K ans;
+    bool ok = true;
     if (hit && (use_cand || !kCompact))
     {
         // The bracket holds the k-th key: radix rounds over the compacted
@@ -458,14 +469,17 @@ __device__ __forceinline__ V select_tracked(const Keys& key, int k,
             }
             ans = radix_select<K, kCompact ? R : 1>(
                     ArrayKeys<K, kCompact ? R : 1>{c}, kk, L, U, n_in, bins,
-                    lane, nprobe);
+                    lane, nprobe, ok);
         }
         else
         {
             ans = radix_select<K, N>(key, kk - c0, L, U, c1 - c0, bins,
-                    lane, nprobe);
+                    lane, nprobe, ok);
         }
         wave_sync();
+        if (!ok)   // bracket bookkeeping broken: search every key
+            ans = search<K, N, true>(key, k, (K)0, kTop, (K)0, kSpan, 0,
+                    nvalid, nprobe);
     }
     else
     {

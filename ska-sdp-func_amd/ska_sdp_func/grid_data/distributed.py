@@ -10,9 +10,15 @@ so each rank grids its own rows and ONE collective combines the ranks:
       images are summed on the destination with torch.distributed.reduce
       (RCCL over xGMI on GPUs). Exact by linearity of FFT, screen and
       correction: (I + sum_r S_r) * C == I * C + sum_r S_r * C.
-  mode="grid": every rank scatters its rows into a private uv grid, the
-      grids are summed on the destination (reduce), which then runs the
-      FFT + screen + correction once (north-star "reduce before FFT").
+  mode="grid": every rank scatters its rows into a private uv grid and
+      the grids are summed on the destination before its column FFTs
+      (north-star "reduce before FFT"). With the fused f32 FFT each rank
+      first runs the row pass of the inverse FFT on its own grid (linear),
+      and only the block the column passes read travels: the row spectra
+      of the Hermitian part, (G/2 + 1) x M complex (178 MB at G 8192, N
+      5440, against the 512 MiB grid); the destination runs the column
+      passes + screen + correction once. Plans without that split (f64,
+      rocFFT grids) reduce the whole grid before one finish.
 
 Degridding needs no collective (replicate the image, shard the rows).
 
@@ -65,11 +71,31 @@ def grid_sharded(gridder, uvw, freq, vis, weight, dirty, dist, mode="image",
         if grid_buf is None:
             raise ValueError("mode='grid' needs grid_buf")
         gridder.grid_scatter(uvw, freq, vis, weight, grid_buf)
-        dist.reduce(grid_buf, dst=dst, group=group)
+        spec = (gridder.row_spectra() if hasattr(gridder, "row_spectra")
+                else None)
+        if spec is None:
+            dist.reduce(grid_buf, dst=dst, group=group)
+            if rank == dst:
+                gridder.grid_finish(grid_buf, dirty)
+            return dirty
+        rows, c0, nc = spec
+        gridder.grid_rows(grid_buf)
+        block = grid_buf[:rows, c0:c0 + nc]
+        packed = block.contiguous() if nc < grid_buf.shape[1] else block
+        dist.reduce(packed, dst=dst, group=group)
         if rank == dst:
-            gridder.grid_finish(grid_buf, dirty)
+            if packed is not block:
+                block.copy_(packed)
+            gridder.grid_finish_rows(grid_buf, dirty)
         return dirty
     raise ValueError(f"unknown mode {mode!r}")
+
+
+def row_spectra_bytes(grid_size, image_size, herm=True, elem_bytes=8):
+    """Bytes of the row-spectra block mode="grid" reduces (fused f32 plans:
+    the (G/2 + 1) x M Hermitian row spectra, M = 2 (N // 2))."""
+    rows = grid_size // 2 + 1 if herm else grid_size
+    return rows * 2 * (image_size // 2) * elem_bytes
 
 
 # Bus bandwidth assumed for one RCCL reduce over the xGMI links of an
@@ -86,16 +112,27 @@ def reduce_ms_model(nbytes, world, bus_gbs=RING_BUS_GBS):
     return (world - 1) / world * nbytes / (bus_gbs * 1e9) * 1e3
 
 
+# HBM rate assumed for the pack / unpack copies of the row-spectra block
+# (a strided torch copy: read + write of the block on each side).
+PACK_GBS = 4000.0
+
+
 def predicted_speedup(t_scatter_ms, t_fft_image_ms, world, grid_bytes,
-                      image_bytes, reduce_ms=None, bus_gbs=RING_BUS_GBS):
+                      image_bytes, reduce_ms=None, bus_gbs=RING_BUS_GBS,
+                      grid_packed=False):
     """Strong-scaling model of one sharded gridding call.
 
     t_scatter_ms: bucketing + tile kernels of the whole call on one GPU (the
     part that divides over the ranks); t_fft_image_ms: FFT + image-plane
-    kernels (once per call in mode "grid", once per rank -- concurrently --
-    in mode "image"). reduce_ms: {"grid": ms, "image": ms} measured at this
-    world size, else the ring model above. Returns {mode: speed-up over one
-    GPU, ...} and the modelled per-call times.
+    kernels (mode "grid": the row pass on every rank concurrently, the
+    column passes once on the destination; mode "image": all of it on
+    every rank, concurrently). grid_bytes: what mode "grid" reduces (the
+    row-spectra block, row_spectra_bytes, or the whole grid); grid_packed:
+    that block is packed into a contiguous buffer and unpacked on the
+    destination (two read + write copies at PACK_GBS). reduce_ms: {"grid":
+    ms, "image": ms} measured at this world size, else the ring model
+    above. Returns {mode: speed-up over one GPU, ...} and the modelled
+    per-call times.
     """
     t1 = t_scatter_ms + t_fft_image_ms
     red = dict(reduce_ms or {})
@@ -104,11 +141,16 @@ def predicted_speedup(t_scatter_ms, t_fft_image_ms, world, grid_bytes,
         r = red.get(mode)
         if r is None:
             r = reduce_ms_model(nbytes, world, bus_gbs)
-        t_n = t_scatter_ms / world + r + t_fft_image_ms
+        pack = (2 * 2 * nbytes / (PACK_GBS * 1e9) * 1e3
+                if mode == "grid" and grid_packed and world > 1 else 0.0)
+        t_n = t_scatter_ms / world + r + pack + t_fft_image_ms
         out[mode] = {"speedup": round(t1 / t_n, 3), "ms": round(t_n, 3),
                      "reduce_ms": round(r, 3),
+                     "reduce_bytes": int(nbytes),
                      "reduce": "measured" if mode in red else
                                f"model ({bus_gbs:.0f} GB/s ring)"}
+        if pack:
+            out[mode]["pack_ms"] = round(pack, 3)
     return out
 
 

@@ -177,6 +177,29 @@ class GridderUvwEsFft(StructWrapper):
         """2-D only: inverse FFT (in place) + screen + correction."""
         Lib.sdp_grid_uvw_es_fft_finish(self, Mem(grid), Mem(dirty_image))
 
+    def row_spectra(self):
+        """(rows, col0, ncols) of the grid block the column passes read
+        after grid_rows, or None if the plan has no fused f32 FFT (f64 or
+        non-power-of-two grids, 3-D). MI355X extension."""
+        r, c, n = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        if not Lib.sdp_gridder_uvw_es_fft_row_spectra(
+                self, ctypes.byref(r), ctypes.byref(c), ctypes.byref(n)):
+            return None
+        return r.value, c.value, n.value
+
+    def grid_rows(self, grid):
+        """First inverse-FFT pass (row FFTs) of a scattered grid, in place.
+        Linear: row spectra of several grids may be summed before
+        grid_finish_rows. MI355X extension."""
+        Lib.sdp_grid_uvw_es_fft_rows(self, Mem(grid))
+
+    def grid_finish_rows(self, grid, dirty_image):
+        """Column passes + screen + correction of a grid after grid_rows:
+        grid_scatter + grid_rows + grid_finish_rows == grid_scatter +
+        grid_finish. MI355X extension."""
+        Lib.sdp_grid_uvw_es_fft_finish_rows(self, Mem(grid),
+                                            Mem(dirty_image))
+
 
 _H = GridderUvwEsFft.handle_type()
 _M = Mem.handle_type()
@@ -213,4 +236,12 @@ Lib.wrap_func("sdp_gridder_uvw_es_fft_get_timing", restype=ctypes.c_int,
 Lib.wrap_func("sdp_grid_uvw_es_fft_scatter", restype=None,
               argtypes=[_H, _M, _M, _M, _M, _M], check_errcode=True)
 Lib.wrap_func("sdp_grid_uvw_es_fft_finish", restype=None,
+              argtypes=[_H, _M, _M], check_errcode=True)
+Lib.wrap_func("sdp_gridder_uvw_es_fft_row_spectra", restype=ctypes.c_int,
+              argtypes=[_H, ctypes.POINTER(ctypes.c_int64),
+                        ctypes.POINTER(ctypes.c_int64),
+                        ctypes.POINTER(ctypes.c_int64)])
+Lib.wrap_func("sdp_grid_uvw_es_fft_rows", restype=None, argtypes=[_H, _M],
+              check_errcode=True)
+Lib.wrap_func("sdp_grid_uvw_es_fft_finish_rows", restype=None,
               argtypes=[_H, _M, _M], check_errcode=True)

@@ -18,11 +18,55 @@ from es_data import make_case, rel_l2
 
 
 class OracleGridder:
-    """CPU stand-in with the GridderUvwEsFft interface (oracle maths)."""
+    """CPU stand-in with the GridderUvwEsFft interface (oracle maths).
 
-    def __init__(self, geo):
+    spectra=True: it also has the row-spectra split of the fused f32 plans
+    (grid_rows / grid_finish_rows / row_spectra) with the real-output
+    layout of es_fft.hip: the row pass transforms the Hermitian part H =
+    (A + conj A(-u, -v)) / 2 of rows 0..G/2 and keeps each row's M centre
+    outputs in columns [0, M); the column pass rebuilds rows G - u as
+    conj(row u) (H is Hermitian, so its row spectra are too)."""
+
+    def __init__(self, geo, spectra=True):
         self.geo = geo
         self.grid_size = geo["grid_size"]
+        self.spectra = spectra
+
+    def _m(self):
+        return 2 * (self.geo["image_size"] // 2)
+
+    def row_spectra(self):
+        if not self.spectra:
+            return None
+        return self.grid_size // 2 + 1, 0, self._m()
+
+    def grid_rows(self, grid):
+        G, M = self.grid_size, self._m()
+        a = grid.numpy()
+        idx = (-np.arange(G)) % G
+        h = 0.5 * (a + np.conj(a[idx][:, idx]))
+        b = np.fft.ifft(h[:G // 2 + 1], axis=1, norm="forward")
+        gc = G // 2
+        grid[:G // 2 + 1, :M] = torch.from_numpy(
+            b[:, gc - M // 2:gc + M // 2].copy())
+
+    def grid_finish_rows(self, grid, dirty):
+        from oracle import es_oracle
+
+        G, M = self.grid_size, self._m()
+        n, half, gc = self.geo["image_size"], self.geo["image_size"] // 2, \
+            self.grid_size // 2
+        bh = grid.numpy()[:G // 2 + 1, :M]
+        full = np.zeros((G, M), complex)
+        full[:G // 2 + 1] = bh
+        full[G // 2 + 1:] = np.conj(bh[1:G // 2][::-1])
+        layer = np.fft.ifft(full, axis=0, norm="forward")
+        off = np.arange(-half, half)
+        sgn = np.where(((off[:, None] + off[None, :]) & 1) != 0, -1.0, 1.0)
+        d = dirty.numpy().astype(np.float64)
+        d[:2 * half, :2 * half] += sgn * layer[gc - half:gc + half].real
+        d[:2 * half, :2 * half] *= es_oracle.correction_map(self.geo)
+        dirty.copy_(torch.from_numpy(d))
 
     def grid_uvw_es_fft(self, uvw, freq, vis, weight, dirty):
         from oracle import es_oracle
@@ -104,8 +148,12 @@ def _worker(rank, world, port, mode, result_path):
             np.save(result_path, np.array([max(
                 rel_l2(dirty.numpy(), ref), rel_l2(dirty2.numpy(), ref2))]))
     else:
-        grid_sharded(OracleGridder(geo), t(uvw[lo:hi]), t(freq),
-                     t(vis[lo:hi]), t(wt[lo:hi]), dirty, dist, mode=mode,
+        # grid_full: a gridder without the row-spectra split (f64 / rocFFT
+        # plans): the whole grids are reduced before one finish.
+        gridder = OracleGridder(geo, spectra=mode != "grid_full")
+        grid_sharded(gridder, t(uvw[lo:hi]), t(freq),
+                     t(vis[lo:hi]), t(wt[lo:hi]), dirty, dist,
+                     mode="grid" if mode == "grid_full" else mode,
                      dst=0, grid_buf=grid_buf)
         if rank == 0:
             ref = es_oracle.grid_uvw_es_fft(geo, uvw, freq, vis, wt,
@@ -115,10 +163,12 @@ def _worker(rank, world, port, mode, result_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["image", "grid", "image_async"])
-def test_sharded_gridding_matches_unsharded(tmp_path, mode):
+@pytest.mark.parametrize("mode,world", [("image", 2), ("grid", 2),
+                                        ("grid", 4), ("grid_full", 2),
+                                        ("image_async", 2)])
+def test_sharded_gridding_matches_unsharded(tmp_path, mode, world):
     path = str(tmp_path / "err.npy")
-    mp.spawn(_worker, args=(2, _free_port(), mode, path), nprocs=2,
+    mp.spawn(_worker, args=(world, _free_port(), mode, path), nprocs=world,
              join=True)
     err = float(np.load(path)[0])
     assert err < 1e-12
@@ -206,6 +256,15 @@ def test_predicted_speedup_model():
     # The image reduce moves 4x fewer bytes than the grid reduce.
     assert p["image"]["speedup"] > p["grid"]["speedup"] > 1.0
     assert p["image"]["speedup"] < 8.0
+    # Mode "grid" reducing the Hermitian row spectra (config 3's G 8192,
+    # N 5440: 178 MB) instead of the 512 MiB grid, with the pack / unpack
+    # copies: the north-star form clears 6x on the config-3 phases.
+    from ska_sdp_func.grid_data.distributed import row_spectra_bytes
+    sb = row_spectra_bytes(8192, 5440)
+    assert sb == 4097 * 5440 * 8
+    q = predicted_speedup(41.5, 0.35, 8, sb, 5440 ** 2 * 4, grid_packed=True)
+    assert q["grid"]["reduce_bytes"] == sb and q["grid"]["pack_ms"] > 0
+    assert 6.0 <= q["grid"]["speedup"] < q["image"]["speedup"]
     m = predicted_speedup(40.0, 0.4, 8, 1 << 29, 1 << 27,
                           reduce_ms={"grid": 2.0})
     assert m["grid"]["reduce"] == "measured"

@@ -44,7 +44,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, mode, result_path):
+def _worker(rank, world, port, mode, n, result_path):
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
@@ -60,7 +60,6 @@ def _worker(rank, world, port, mode, result_path):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
-    n = 512
     uvw, freq, vis, wt, px = make_case(41, 20011, 4, n)
     dirty_in = np.random.default_rng(7).standard_normal((n, n)).astype(
         np.float32)
@@ -70,6 +69,17 @@ def _worker(rank, world, port, mode, result_path):
     plan = GridderUvwEsFft(g(uvw), g(freq), g(vis), g(wt), dirty, px, px,
                            1e-5, False)
     G = plan.grid_size
+    if mode == "grid":
+        # n 512: grid 770 (rocFFT, whole-grid reduce); n 680: grid 1024,
+        # complex row pass (every row reduced); n 1360: grid 2048,
+        # real-output row pass (the G/2 + 1 Hermitian rows reduced).
+        spec = plan.row_spectra()
+        if G & (G - 1):
+            assert spec is None
+        else:
+            rows, c0, nc = spec
+            assert (c0, nc) == (0, 2 * (n // 2))
+            assert rows == (G // 2 + 1 if 2048 <= G <= 8192 else G)
     grid_buf = torch.zeros((G, G), dtype=torch.complex64, device=dev)
     grid_sharded(plan, g(uvw[lo:hi]), g(freq), g(vis[lo:hi]), g(wt[lo:hi]),
                  dirty, HostStagedDist(), mode=mode, dst=0,
@@ -88,10 +98,11 @@ def _worker(rank, world, port, mode, result_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["image", "grid"])
-def test_sharded_gridding_on_gpu_matches_oracle(tmp_path, mode):
+@pytest.mark.parametrize("mode,n", [("image", 512), ("grid", 512),
+                                    ("grid", 680), ("grid", 1360)])
+def test_sharded_gridding_on_gpu_matches_oracle(tmp_path, mode, n):
     path = str(tmp_path / "err.npy")
-    ctx = mp.spawn(_worker, args=(2, _free_port(), mode, path), nprocs=2,
+    ctx = mp.spawn(_worker, args=(2, _free_port(), mode, n, path), nprocs=2,
                    join=False)
     deadline = time.time() + 240
     while not ctx.join(timeout=5):

@@ -190,6 +190,25 @@ def test_grid_all_is_adjoint_and_shards_sum(device):
         vacc += vpart
     _close(acc.cpu().numpy(), gy.cpu().numpy(), 1e-10, border=128)
     _close(vacc.cpu().numpy(), ax.cpu().numpy(), 1e-12)
+    # A mask range that misses occupied planes at both ends (a plane-range
+    # model that is off): the planes outside belong to the owners of the
+    # first / last entry, so the shards still sum to the whole.
+    cut = masks[:, 2:-2]
+    assert cut.shape[1] >= 1 and loads[1] + loads[-2] > 0
+    acc.zero_()
+    vacc.zero_()
+    for k in range(3):
+        part = torch.zeros_like(gy)
+        g.wstack_wtower_grid_plane_set(dev(y), a[0], a[1], d_uvw, *a[3:], 0,
+                                       part, first + 2, dev(cut[k]))
+        acc += part
+        vpart = torch.zeros_like(ax)
+        g.wstack_wtower_degrid_plane_set(dev(x), a[0], a[1], d_uvw, *a[3:],
+                                         0, vpart, first + 2,
+                                         np.ascontiguousarray(cut[k]))
+        vacc += vpart
+    _close(acc.cpu().numpy(), gy.cpu().numpy(), 1e-10, border=128)
+    _close(vacc.cpu().numpy(), ax.cpu().numpy(), 1e-12)
 
 
 def test_argument_errors(device, case):
