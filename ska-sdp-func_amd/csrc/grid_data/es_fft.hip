@@ -15,10 +15,12 @@
 // e * B + column.
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
 #include "es_fft.h"
+#include "es_fft_wstack.h"
 #include "es_image_dev.h"
 #include "../utility/sdp_hip.h"
 
@@ -1472,6 +1474,98 @@ k_rows_image_herm1(float2* __restrict__ grid, int k0, int M,
     }
 }
 
+// W-stacking image side (w-towers gridder, sdp_grid_wstack_wtower.hip) -------
+//
+// Gridding a w-stack plane ends with: gather the FFT'd sub-grids of the
+// plane into the G x G grid (k_gather_grid), inverse FFT of the grid
+// (rows, then the four-step columns), then image += grid_correct(checker(
+// IFFT) / G^2) (k_image_update; ref sdp_grid_wstack_wtower.cpp:686-711).
+// The kernel below fuses the image update into the last column pass: the
+// grid is then written once less (by that pass) and read once less (by
+// the image update), 2 GiB each at G = 16384.
+
+// Column pass B (inverse) with the image update: for k2 = blockIdx.x,
+// length-N1 FFTs over rows N1 * k2 + n1; natural output row gu = k2 + N2 k1,
+// column gv: image[gu][gv] += correct(checker * x * norm) in the order and
+// precision of k_image_update (sdp_grid_wstack_wtower.hip; the correction
+// of a float grid, correct_scaled_f32: scale in f32, then the w-stack
+// phasor of w_offset).
+// IK: the image's element kind (AnyView: 0 f32, 1 f64, 2 c64, 3 c128).
+template<int N1, int N2, int IK>
+__global__ void __launch_bounds__(256)
+k_cols_b_wstack_image(const float2* __restrict__ grid, void* image_ptr,
+        float norm, sdp_wt::CorrParams cp, const float2* __restrict__ W)
+{
+#pragma clang fp contract(off)
+    constexpr int G = N1 * N2, B = ColPlan<N1>::B;
+    constexpr int kGridKind = 2;                  // complex float grid
+    using F = ColFft<N1, 1>;
+    using R = typename std::conditional<(IK == 1 || IK == 3), double,
+            float>::type;
+    constexpr bool kCx = IK >= 2;
+    extern __shared__ float2 lds[];
+    const int c = threadIdx.x % B, p = threadIdx.x / B;
+    const int k2 = blockIdx.x;
+    const Buf gb(grid, grid_bytes(G, 0));
+    R* img = (R*)image_ptr;
+    F f;
+    f.init(p, W, G);
+    const int ncb = G / B;
+    const uint32_t so = (uint32_t)N1 * k2 * G * 8u;
+    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
+    {
+        const int pq = opaque(p), cq = opaque(c);
+        const int col = cb * B + cq;
+        const uint32_t vo = ((uint32_t)pq * G + col) * 8u;
+        float2 v[F::EPT];
+        F::load_input(v, [&](int e) {
+            return gb.load(vo, so + e * (uint32_t)G * 8u);
+        });
+        // The image values and correction scales of this thread's outputs,
+        // loaded ahead of the transform (these passes are latency-bound).
+        const int pm = col - G / 2;
+        R prev_re[F::EPT], prev_im[kCx ? F::EPT : 1];
+        float sc[F::EPT];
+#pragma unroll
+        for (int i = 0; i < F::EPT; ++i)
+        {
+            const int64_t gu = k2 + (int64_t)N2 * F::out_index(pq, i);
+            const int64_t idx = gu * G + col;
+            prev_re[i] = img[kCx ? 2 * idx : idx];
+            if constexpr (kCx) prev_im[i] = img[2 * idx + 1];
+            const int pl = (int)(gu - G / 2);
+            sc[i] = sdp_wt::corr_inside(pl, pm, cp) ?
+                    (float)sdp_wt::corr_scale(pl, pm, kGridKind, cp) : 1.0f;
+        }
+        f.transform(v, pq, lds, ColIdx<B>{cq});
+        F::store_output(v, [&](int e, int i, float2 x) {
+            const int64_t gu = k2 + (int64_t)N2 * (pq + e);
+            float re = x.x, im = x.y;
+            if ((gu + col) & 1)
+            {
+                re = -re;
+                im = -im;
+            }
+            re *= norm;
+            im *= norm;
+            sdp_wt::Cx<double> z = sdp_wt::cx<double>(re, im);
+            const int pl = (int)(gu - G / 2);
+            if (sdp_wt::corr_inside(pl, pm, cp))
+                z = sdp_wt::correct_scaled_f32(z, pl, pm, cp, sc[i]);
+            const int64_t idx = gu * G + col;
+            if constexpr (kCx)
+            {
+                img[2 * idx] = (R)((double)prev_re[i] + z.re);
+                img[2 * idx + 1] = (R)((double)prev_im[i] + z.im);
+            }
+            else
+            {
+                img[idx] = (R)((double)prev_re[i] + z.re);
+            }
+        });
+    }
+}
+
 // Launch helpers --------------------------------------------------------------
 
 int num_cus()
@@ -1851,6 +1945,42 @@ int fft2d_block(float2* grid, bool forward, const float2* W,
     return st;
 }
 
+// Inverse FFT of a w-stack plane with the image update fused into the
+// last column pass.
+template<int N1, int N2>
+int wstack_grid_image(float2* grid, const sdp_wt::AnyView& image, float norm,
+        const sdp_wt::CorrParams& cp, const float2* W, hipStream_t stream)
+{
+    constexpr int G = N1 * N2;
+    sdp_Error st = SDP_SUCCESS;
+    const size_t lds = row_lds_bytes(G);
+    SDP_HIP_CHECK((allow_lds<k_rows_grid<G>>(lds)), &st);
+    if (st) return st;
+    k_rows_grid<G><<<row_blocks(G), RowPlan<G>::P, lds, stream>>>(
+            grid, 0, G, W, nullptr, 0);
+    SDP_HIP_CHECK_LAUNCH(&st);
+    if (st) return st;
+    k_cols_a_grid<N1, N2, 1><<<col_grid<k_cols_a_grid<N1, N2, 1>>(N1, G,
+            ColPlan<N2>::B), 256, kColLdsBytes, stream>>>(grid, G, W);
+    SDP_HIP_CHECK_LAUNCH(&st);
+    if (st) return st;
+#define SDP_WS_COLB(IK) \
+    k_cols_b_wstack_image<N1, N2, IK><<<col_grid<k_cols_b_wstack_image<N1, \
+            N2, IK>>(N2, G, ColPlan<N1>::B), 256, kColLdsBytes, stream>>>( \
+            grid, image.ptr, norm, cp, W)
+    switch (image.kind)
+    {
+    case 0: SDP_WS_COLB(0); break;
+    case 1: SDP_WS_COLB(1); break;
+    case 2: SDP_WS_COLB(2); break;
+    case 3: SDP_WS_COLB(3); break;
+    default: return SDP_ERR_INVALID_ARGUMENT;
+    }
+#undef SDP_WS_COLB
+    SDP_HIP_CHECK_LAUNCH(&st);
+    return st;
+}
+
 // Dispatch on G = N1 * N2 (N2 = N1 or 2 * N1).
 #define SDP_ES_FFT_DISPATCH(G, CALL) \
     switch (G) \
@@ -2003,6 +2133,16 @@ int fft2d_inplace_permuted(float* grid, int grid_size, bool forward,
     const float2* W = (const float2*)tw.table;
     SDP_ES_FFT_DISPATCH(grid_size, (fft2d_block<N1, N2>((float2*)grid,
             forward, W, stream)))
+}
+
+int fft2d_wstack_grid_image(float* grid, int grid_size, const FftTwiddles& tw,
+        const sdp_wt::AnyView& image, float norm,
+        const sdp_wt::CorrParams& cp, hipStream_t stream)
+{
+    if (tw.G != grid_size) return SDP_ERR_INVALID_ARGUMENT;
+    const float2* W = (const float2*)tw.table;
+    SDP_ES_FFT_DISPATCH(grid_size, (wstack_grid_image<N1, N2>((float2*)grid,
+            image, norm, cp, W, stream)))
 }
 
 int fft_perm_n2(int grid_size)

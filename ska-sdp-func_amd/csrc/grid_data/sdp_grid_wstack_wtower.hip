@@ -53,6 +53,7 @@
 #include "wtower_plan.h"
 #include "../fft/fft2d.h"
 #include "es_fft.h"
+#include "es_fft_wstack.h"
 #include "../utility/sdp_hip.h"
 
 using namespace sdp_wt;
@@ -641,16 +642,6 @@ __global__ void k_cut_out(const Cx<T>* __restrict__ grid, int64_t G,
     }
 }
 
-// floor(x / d) for d > 0 and |x| < 2^24: a float estimate, corrected once.
-__device__ __forceinline__ int floor_div_small(int x, int d, float inv_d)
-{
-    int q = (int)floorf((float)x * inv_d);
-    const int r = x - q * d;
-    if (r < 0) --q;
-    else if (r >= d) ++q;
-    return q;
-}
-
 // Gridding: grid (+)= sum of the FFT'd sub-grids covering each cell, in
 // the reference's task order (sdp_gridder_subgrid_add, utils.cpp:553-601,
 // sequential over tasks), with the sub-grid FFT's output checkerboard, the
@@ -676,31 +667,12 @@ __global__ void k_gather_grid(Cx<T>* __restrict__ grid, int64_t G64,
     if (gv >= G) return;
     const int64_t gi = (int64_t)gu * G + gv;
     const float inv_eff = 1.0f / (float)eff;
-    // Candidates along one axis, ascending (wrap k = -1, 0, 1, then index).
-    auto candidates = [&](int x0, int lo_idx, int n_idx, int (&off)[kGatherCand],
-            int (&idx)[kGatherCand]) {
-        int nc = 0;
-        for (int k = -1; k <= 1; ++k)
-        {
-            const int x = x0 + k * G;
-            const int i_lo = max(floor_div_small(x - S + eff, eff, inv_eff),
-                    lo_idx);
-            const int i_hi = min(floor_div_small(x, eff, inv_eff),
-                    lo_idx + n_idx - 1);
-            for (int ii = i_lo; ii <= i_hi; ++ii)
-            {
-                const int o = x - ii * eff;
-                if (o < 0 || o >= S || nc >= kGatherCand) continue;
-                off[nc] = o;
-                idx[nc] = ii - lo_idx;
-                ++nc;
-            }
-        }
-        return nc;
-    };
+    // Candidates along each axis, ascending (wrap k = -1, 0, 1, then index).
     int ua[kGatherCand], uu[kGatherCand], vb[kGatherCand], vv[kGatherCand];
-    const int nuc = candidates(gu - G / 2 + S / 2, min_iu, nu, ua, uu);
-    const int nvc = candidates(gv - G / 2 + S / 2, min_iv, nv, vb, vv);
+    const int nuc = gather_candidates(gu - G / 2 + S / 2, G, S, eff, inv_eff,
+            min_iu, nu, ua, uu);
+    const int nvc = gather_candidates(gv - G / 2 + S / 2, G, S, eff, inv_eff,
+            min_iv, nv, vb, vv);
     constexpr int kC = kGatherCand * kGatherCand;
     int slot[kC];
 #pragma unroll
@@ -796,7 +768,8 @@ __global__ void k_image_update(const Cx<T>* __restrict__ grid, int64_t G,
         const int pl = (int)(gu - G / 2);
         Cx<double> z = cx<double>(v.re, v.im);
         if (corr_inside(pl, pm, cp))
-            z = correct_scaled(z, kind, pl, pm, cp, sc[r]);
+            z = (kind == 2) ? correct_scaled_f32(z, pl, pm, cp, (float)sc[r]) :
+                    correct_scaled(z, kind, pl, pm, cp, sc[r]);
         Cx<double> out = o[r];
         out.re += z.re;
         if (image.kind >= 2) out.im += z.im;
@@ -836,7 +809,8 @@ __global__ void k_image_to_grid(AnyView image, int64_t G,
         const int pl = (int)(gu - G / 2);
         Cx<double> z = cx<double>((double)(T)a[r].re, (double)(T)a[r].im);
         if (corr_inside(pl, pm, cp))
-            z = correct_scaled(z, kind, pl, pm, cp, sc[r]);
+            z = (kind == 2) ? correct_scaled_f32(z, pl, pm, cp, (float)sc[r]) :
+                    correct_scaled(z, kind, pl, pm, cp, sc[r]);
         T re = (T)z.re, im = (T)z.im;
         if (parity_sign(gu + gv) < 0)
         {
@@ -2475,6 +2449,17 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
             return (int)(((g.S + g.eff - 1) / g.eff) * wraps);
         };
         const int ncand = std::max(axis_cand(g.nu), axis_cand(g.nv));
+        // The plane's last group with the fused f32 plane FFT: the image
+        // update runs inside the FFT's last column pass (es_fft_wstack.h).
+        // (A gather fused into the row pass measured 10.3 ms per plane at
+        // config 4 against 2.0 + 0.9 ms for the gather and the row pass:
+        // one 512-thread workgroup per CU cannot hide the dependent
+        // slot-table and sub-grid loads; the gather stays its own pass.)
+        static const bool ab_sep = getenv("SDP_WS_AB_SEPARATE") != nullptr;
+        const sdp_es::FftTwiddles* tw_plane = (gr.last_of_plane &&
+                sizeof(T) == 4 && !ab_sep) ? plane_fft_twiddles(G, false,
+                status) : nullptr;
+        if (*status) break;
         if (ncand <= 3)
             k_gather_grid<T, 3><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
                     d_grid, G, d_stack, g.S, d_slot_of + gi * g.ntask, g.nu,
@@ -2498,7 +2483,23 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
             (void)hipDeviceSynchronize();
             tm.towers += now_s() - tg;
         }
-        if (gr.last_of_plane)
+        if (gr.last_of_plane && tw_plane)
+        {
+            const double ti = now_s();
+            const CorrParams cp = corr_params_tab(k, (int)(gr.iw * g.H), true,
+                    true, status);
+            if (*status) break;
+            const int e = sdp_es::fft2d_wstack_grid_image((float*)d_grid,
+                    (int)G, *tw_plane, image,
+                    (float)(1.0 / ((double)G * G)), cp, 0);
+            if (e) { *status = (sdp_Error)e; break; }
+            if (verbosity > 0)
+            {
+                (void)hipDeviceSynchronize();
+                tm.image += now_s() - ti;
+            }
+        }
+        else if (gr.last_of_plane)
         {
             const double ti = now_s();
             const sdp_es::FftTwiddles* tw = plane_fft_twiddles(G,
@@ -2627,18 +2628,27 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
             const double ti = now_s();
             const CorrParams cp = corr_params_tab(k, (int)(gr.iw * g.H),
                     false, sizeof(T) == 4, status);
-            k_image_to_grid<T><<<dim3(blocks_of(G),
-                    (unsigned)((G + kImgRows - 1) / kImgRows)), 256>>>(
-                    image, G, d_grid, cp);
-            SDP_HIP_CHECK_LAUNCH(status);
+            // (The image prologue fused into the plane FFT's row pass,
+            // es_fft_wstack.h, measured 3.5 ms per plane at config 4
+            // against 1.8 + 0.9 ms for the two passes: the per-element
+            // double-precision correction starves the row pass's one
+            // workgroup per CU.)
             if (tw)
             {
+                k_image_to_grid<T><<<dim3(blocks_of(G),
+                        (unsigned)((G + kImgRows - 1) / kImgRows)), 256>>>(
+                        image, G, d_grid, cp);
+                SDP_HIP_CHECK_LAUNCH(status);
                 const int e = sdp_es::fft2d_inplace_permuted((float*)d_grid,
                         (int)G, true, *tw, 0);
                 if (e) *status = (sdp_Error)e;
             }
             else
             {
+                k_image_to_grid<T><<<dim3(blocks_of(G),
+                        (unsigned)((G + kImgRows - 1) / kImgRows)), 256>>>(
+                        image, G, d_grid, cp);
+                SDP_HIP_CHECK_LAUNCH(status);
                 sdp_fft::exec_2d(big, d_grid, true, 0, status);
             }
             if (verbosity > 0)

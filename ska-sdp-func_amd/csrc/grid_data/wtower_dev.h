@@ -188,6 +188,46 @@ __device__ __forceinline__ double lm_to_n_dev(double l, double m, double h_u,
     return (sqrt(a * a - b * (l * l + m * m)) + a) / b;
 }
 
+// floor(x / d) for d > 0 and |x| < 2^24: a float estimate, corrected once.
+__device__ __forceinline__ int floor_div_small(int x, int d, float inv_d)
+{
+    int q = (int)floorf((float)x * inv_d);
+    const int r = x - q * d;
+    if (r < 0) --q;
+    else if (r >= d) ++q;
+    return q;
+}
+
+// Sub-grids along one axis that cover grid cell x0 (relative to the first
+// sub-grid origin, G/2 - S/2 cells from the grid's first cell), in the
+// reference's task order (wrap k = -1, 0, 1, then index; utils.cpp:553-601):
+// off[] the cell's offset inside each, idx[] its sub-grid index minus
+// lo_idx; returns how many (at most NC, host-checked).
+template<int NC>
+__device__ __forceinline__ int gather_candidates(int x0, int G, int S,
+        int eff, float inv_eff, int lo_idx, int n_idx, int (&off)[NC],
+        int (&idx)[NC])
+{
+    int nc = 0;
+    for (int k = -1; k <= 1; ++k)
+    {
+        const int x = x0 + k * G;
+        const int i_lo = max(floor_div_small(x - S + eff, eff, inv_eff),
+                lo_idx);
+        const int i_hi = min(floor_div_small(x, eff, inv_eff),
+                lo_idx + n_idx - 1);
+        for (int ii = i_lo; ii <= i_hi; ++ii)
+        {
+            const int o = x - ii * eff;
+            if (o < 0 || o >= S || nc >= NC) continue;
+            off[nc] = o;
+            idx[nc] = ii - lo_idx;
+            ++nc;
+        }
+    }
+    return nc;
+}
+
 } // namespace sdp_wt
 
 #endif

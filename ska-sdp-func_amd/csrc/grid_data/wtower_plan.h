@@ -170,6 +170,42 @@ __device__ __forceinline__ Cx<double> correct_scaled(Cx<double> z, int kind,
     return z;
 }
 
+// correct_scaled for a complex-float grid (kind 2) in the image-side passes
+// of the w-stack imager (k_image_update, k_image_to_grid, the fused column
+// pass of es_fft_wstack.h): the same f32 scale and f32 complex product; the
+// w-stack phase w_step n w_offset is formed and reduced to [-1/2, 1/2]
+// turns in double as there, but its sine and cosine are taken in single
+// precision (sincospif of the reduced phase, ~1 ulp of the f32 values
+// correct_scaled rounds its double ones to) instead of double sincospi:
+// the double trigonometry was most of those passes' time at config 4
+// (1.9 ms per 16384^2 plane).
+__device__ __forceinline__ Cx<double> correct_scaled_f32(Cx<double> z, int pl,
+        int pm, const CorrParams& cp, float scale)
+{
+#pragma clang fp contract(off)
+    float zr = (float)z.re * scale;
+    float zi = (float)z.im * scale;
+    if (cp.w_offset != 0)
+    {
+        // Pixel size and w_step w_offset as one factor each (no double
+        // division per pixel; the phase moves by ~1 ulp of a double).
+        const double px = cp.theta / cp.image_size;
+        const double l = pl * px;
+        const double m = pm * px;
+        const double n = lm_to_n_dev(l, m, cp.shear_u, cp.shear_v);
+        const double turns = (cp.w_step * cp.w_offset) * n;
+        float sn, cs;
+        sincospif(2.0f * (float)(turns - rint(turns)), &sn, &cs);
+        // |w| = 1: 1 / w = conj(w) (degrid_correct).
+        const float wr = cs, wi = cp.inverse ? sn : -sn;
+        const float xr = zr * wr - zi * wi;
+        const float xi = zr * wi + zi * wr;
+        zr = xr;
+        zi = xi;
+    }
+    return cx<double>(zr, zi);
+}
+
 // Pixel (pl, pm) relative to the image centre of a facet of element kind
 // `kind` (AnyView): 1 / (pswf(l) pswf(m) pswf_n(n)), then, for complex
 // facets, the w-stacking phasor exp(+-2 pi i w_step n w_offset)

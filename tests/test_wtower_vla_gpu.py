@@ -213,3 +213,67 @@ def test_run_and_check(device, reference, loc, uvw_t, vis_t, img_t,
                        rtol=1e-6)
     print(f", rms image {rms_img:.3e}")
     assert rms_img < 1e-3
+
+
+def test_fused_plane_image_kinds_agree(device, reference):
+    """The fused image side of a complex-float plane (the sub-grid gather
+    in the plane FFT's row pass, the corrected image update in its last
+    column pass; es_fft_wstack.h) writes every image kind: the f32 image
+    is Re of the c64 one, the c128 image the c64 one in double, all from
+    the same c64 visibilities at grid 1024 (the c64 image is pinned to the
+    reference recipe by test_run_and_check)."""
+    import torch
+    import ska_sdp_func.grid_data as g
+
+    grid_size = 1024
+    theta, w_step, H = _geometry(grid_size, reference["fov"],
+                                 reference["cell"])
+    put = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    uvw = put(reference["uvw"].astype(np.float32))
+    vis = put(reference["ref_vis"].astype(np.complex64))
+    common = (FREQ0, DFREQ, uvw, SUBGRID, theta, w_step, 0.0, 0.0, 8,
+              16 * 1024, 8, 16 * 1024, 2.0 / 3.0, H, 0)
+    out = {}
+    for t in (np.complex64, np.complex128, np.float32, np.float64):
+        img = put(np.full((grid_size, grid_size), 0.25, t))  # overwritten
+        g.wstack_wtower_grid_all(vis, *common[:2], common[2], *common[3:],
+                                 img)
+        out[t] = img.cpu().numpy().astype(np.complex128)
+    ref = out[np.complex64]
+    scale = np.max(np.abs(ref))
+    assert np.max(np.abs(out[np.complex128] - ref)) <= 2e-6 * scale
+    assert np.max(np.abs(out[np.float32] - ref.real)) <= 2e-6 * scale
+    assert np.max(np.abs(out[np.float64] - ref.real)) <= 2e-6 * scale
+    assert np.count_nonzero(out[np.float32].imag) == 0
+
+
+def test_fused_plane_degrid_image_kinds_agree(device, reference):
+    """Degridding through the fused image prologue (the degrid correction
+    and checkerboard in the plane FFT's row pass, es_fft_wstack.h) reads
+    every image kind: a real image gives the same visibilities as f32, f64,
+    c64 or c128, from the reference model at grid 1024 (the c64 case is
+    pinned to the reference recipe by test_run_and_check)."""
+    import torch
+    import ska_sdp_func.grid_data as g
+
+    grid_size = 1024
+    theta, w_step, H = _geometry(grid_size, reference["fov"],
+                                 reference["cell"])
+    put = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    uvw = put(reference["uvw"].astype(np.float32))
+    rows = len(reference["uvw"])
+    common = (FREQ0, DFREQ, uvw, SUBGRID, theta, w_step, 0.0, 0.0, 8,
+              16 * 1024, 8, 16 * 1024, 2.0 / 3.0, H, 0)
+    out = {}
+    for t in (np.complex64, np.complex128, np.float32, np.float64):
+        img = np.zeros((grid_size, grid_size), t)
+        g.subgrid_add(img, 0, 0, reference["model"].astype(t), 1.0)
+        vis = put(np.zeros((rows, NUM_CHAN), np.complex64))
+        g.wstack_wtower_degrid_all(put(img), *common[:2], common[2],
+                                   *common[3:], vis)
+        out[t] = vis.cpu().numpy().astype(np.complex128)
+    ref = out[np.complex64]
+    scale = np.max(np.abs(ref))
+    assert scale > 0
+    for t in (np.complex128, np.float32, np.float64):
+        assert np.max(np.abs(out[t] - ref)) <= 2e-6 * scale, t
