@@ -18,6 +18,9 @@ if [[ $PARTS == *test* ]]; then
         --timeout-method thread > "$OUT/pytest.log" 2>&1 \
         || { tail -40 "$OUT/pytest.log"; exit 1; }
     tail -1 "$OUT/pytest.log"
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" \
+        > "$OUT/smoke.log" 2>&1 || { tail -20 "$OUT/smoke.log"; exit 1; }
+    tail -1 "$OUT/smoke.log"
 fi
 if [[ $PARTS == *es* ]]; then
     timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
@@ -39,6 +42,9 @@ fi
 if [[ $PARTS == *traffic* ]]; then
     scripts/pmc_traffic.sh "$OUT/traffic" --steps 3 --warmup 1 \
         --no-cpu-baseline --no-degrid --no-config3 --no-wstack || exit 1
+    python3 scripts/pmc_traffic.py "$OUT/traffic" "$OUT/pmc_traffic.json" \
+        > /dev/null || exit 1
+    find "$OUT/traffic" -name "*.csv" ! -name "*counter_collection.csv" -delete
 fi
 if [[ $PARTS == *wt* ]]; then
     timeout -k 10 600 python -u bench_wtower.py --degrid > "$OUT/wtower.json" \
@@ -53,5 +59,9 @@ if [[ $PARTS == *flag* ]]; then
     timeout -k 10 600 python -u bench_flagger.py > "$OUT/flagger.json" \
         2> "$OUT/flagger.err" || { tail -20 "$OUT/flagger.err"; exit 1; }
     tail -c 400 "$OUT/flagger.json"; echo
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$OUT/fkt" -o fl -- python3 bench_flagger.py --steps 2 --warmup 1 \
+        --no-cpu-baseline > "$OUT/fkt.log" 2>&1 || { tail -5 "$OUT/fkt.log"; exit 1; }
+    stats "$OUT/fkt" flagger_kernel_stats.csv || exit 1
 fi
 echo measure done

@@ -8,7 +8,7 @@ cd "$(dirname "$0")/../ska-sdp-func_amd"
 D=/tmp/kst/$(basename "$SRC")
 mkdir -p "$D"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 \
-    -munsafe-fp-atomics -I../include -Icsrc -x hip -c "$SRC" \
+    -munsafe-fp-atomics $KFLAGS -I../include -Icsrc -x hip -c "$SRC" \
     --save-temps=obj -o "$D/out.o" 2> /dev/null || \
   (cd "$D" && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 \
     -munsafe-fp-atomics -I"$OLDPWD/../include" -I"$OLDPWD/csrc" -x hip -c \

@@ -2455,10 +2455,9 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
         // config 4 against 2.0 + 0.9 ms for the gather and the row pass:
         // one 512-thread workgroup per CU cannot hide the dependent
         // slot-table and sub-grid loads; the gather stays its own pass.)
-        static const bool ab_sep = getenv("SDP_WS_AB_SEPARATE") != nullptr;
         const sdp_es::FftTwiddles* tw_plane = (gr.last_of_plane &&
-                sizeof(T) == 4 && !ab_sep) ? plane_fft_twiddles(G, false,
-                status) : nullptr;
+                sizeof(T) == 4) ? plane_fft_twiddles(G, false, status) :
+                nullptr;
         if (*status) break;
         if (ncand <= 3)
             k_gather_grid<T, 3><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
