@@ -368,33 +368,22 @@ __global__ __launch_bounds__(NT) void k_bucket_count(EsParams<T> p,
 }
 
 // Per bin: exclusive prefix over chunks (in place) and the bin total.
-// Block = 16 waves; lane = bin, wave = contiguous range of chunks. One
-// launch scans two tables: blocks [0, nblk) the first, the rest the second.
-__global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
-        int num_chunks, int nbins, uint32_t* __restrict__ bin_count,
-        int nblk, uint32_t* table2, int num_chunks2, int nbins2,
-        uint32_t* __restrict__ bin_count2)
+// Block = 16 waves; lane = bin, wave = contiguous range of chunks. MAXPER:
+// rows per wave the registers hold (a uniform bound: the group table's 64
+// rows at config 2 take 4 loads per thread, the chunk table's up to 1024
+// rows 64; one bound for both issued 60 out-of-range loads per thread on
+// the group table, 17.5 us per call).
+template<int MAXPER>
+__device__ __forceinline__ void scan_columns_block(uint32_t* table,
+        int num_chunks, int nbins, uint32_t* __restrict__ bin_count, int bx,
+        uint32_t (&part)[16][64])
 {
     // nbins = columns = the table row length (tile and super-bin counts).
-    __shared__ uint32_t part[16][64];
-    int bx = blockIdx.x;
-    if (bx >= nblk)
-    {
-        table = table2;
-        num_chunks = num_chunks2;
-        nbins = nbins2;
-        bin_count = bin_count2;
-        bx -= nblk;
-    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = bx * 64 + lane;
     const int per = (num_chunks + 15) / 16;
     const int c0 = __builtin_amdgcn_readfirstlane(wave * per);
     const int c1 = min(num_chunks, c0 + per);
-    // The wave's column of counts stays in registers between the two
-    // passes (the table is read once: 64 MiB at config 2).
-    constexpr int kMaxPer = kMaxChunks / 16;
-    static_assert(kMaxChunks % 16 == 0, "chunks split over 16 waves");
     // Raw buffer view of the table: lane offset (bin) in one VGPR, chunk
     // offset in an SGPR; lanes past nbins and chunks past c1 address out of
     // range (loads return 0, stores are dropped).
@@ -404,10 +393,12 @@ __global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
     auto soff = [&](int k) -> uint32_t {
         return c0 + k < c1 ? (uint32_t)((c0 + k) * nbins) * 4u : 0x7FFFFFF0u;
     };
-    uint32_t val[kMaxPer];
+    // The wave's column of counts stays in registers between the two
+    // passes (the table is read once).
+    uint32_t val[MAXPER];
     uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < kMaxPer; ++k)
+    for (int k = 0; k < MAXPER; ++k)
     {
         val[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, voff,
                 soff(k), 0);
@@ -431,12 +422,41 @@ __global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
     {
         uint32_t run = part[wave][lane];
 #pragma unroll
-        for (int k = 0; k < kMaxPer; ++k)
+        for (int k = 0; k < MAXPER; ++k)
         {
             __builtin_amdgcn_raw_buffer_store_b32(run, rs, voff, soff(k), 0);
             run += val[k];
         }
     }
+}
+
+// One launch scans two tables: blocks [0, nblk) the first, the rest the
+// second, each with the register bound of its row count.
+__global__ __launch_bounds__(1024) void k_scan_columns(uint32_t* table,
+        int num_chunks, int nbins, uint32_t* __restrict__ bin_count,
+        int nblk, uint32_t* table2, int num_chunks2, int nbins2,
+        uint32_t* __restrict__ bin_count2)
+{
+    __shared__ uint32_t part[16][64];
+    constexpr int kMaxPer = kMaxChunks / 16;
+    static_assert(kMaxChunks % 16 == 0, "chunks split over 16 waves");
+    int bx = blockIdx.x;
+    if (bx >= nblk)
+    {
+        table = table2;
+        num_chunks = num_chunks2;
+        nbins = nbins2;
+        bin_count = bin_count2;
+        bx -= nblk;
+    }
+    const int per = (num_chunks + 15) / 16;   // uniform per block
+    if (per <= 4)
+        scan_columns_block<4>(table, num_chunks, nbins, bin_count, bx, part);
+    else if (per <= 16)
+        scan_columns_block<16>(table, num_chunks, nbins, bin_count, bx, part);
+    else
+        scan_columns_block<kMaxPer>(table, num_chunks, nbins, bin_count, bx,
+                part);
 }
 
 // Exclusive prefix of bin totals and of work items (pieces of <= kPiece

@@ -195,3 +195,29 @@ def test_plane_fft_permuted_vs_numpy(device, G, forward):
     err = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
     print(f"plane FFT G {G} forward {forward}: rel-L2 {err:.2e}")
     assert err < 1e-5
+
+
+def test_plane_fft_twiddles_per_device(device):
+    """The permuted plane FFT keeps its twiddle tables per (device, G): a
+    transform on a second GPU after one on the first must use tables in its
+    own memory (advisor finding, round 5). Runs on every visible device in
+    turn, against numpy; with one GPU it checks the per-device key on
+    device 0 twice."""
+    import torch
+    from ska_sdp_func.fourier_transforms import (fft_2d_inplace_permuted,
+                                                 fft_permuted_n2)
+
+    G = 1024
+    n2 = fft_permuted_n2(G)
+    k = np.arange(G)
+    rng = np.random.default_rng(11)
+    host = (rng.standard_normal((G, G)) + 1j * rng.standard_normal((G, G)))
+    ref = np.fft.fft2(host)
+    devs = list(range(torch.cuda.device_count())) or [0]
+    for d in devs + devs[:1]:
+        with torch.cuda.device(d):
+            x = torch.from_numpy(host.astype(np.complex64)).to(f"cuda:{d}")
+            fft_2d_inplace_permuted(x, True)
+            got = x.cpu().numpy()[(G // n2) * (k % n2) + k // n2]
+        err = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+        assert err < 1e-5, (d, err)
