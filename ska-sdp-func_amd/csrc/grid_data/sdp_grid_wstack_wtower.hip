@@ -610,12 +610,16 @@ __global__ void k_cut_out(const Cx<T>* __restrict__ grid, int64_t G,
             if (a0 + r < S) out[(int64_t)(a0 + r) * S] = cx<T>(0, 0);
         return;
     }
+    // 32-bit index arithmetic (G < 2^30, tasks < 2^31; host-checked): the
+    // int64 divisions here were ~450 scalar instructions per wave.
     const int t = task[slot];
-    const int64_t iu = min_iu + t / nv, iv = min_iv + t % nv;
-    int64_t ou = (G / 2 - S / 2 + iu * eff) % G;
-    int64_t ov = (G / 2 - S / 2 + iv * eff) % G;
-    if (ou < 0) ou += G;
-    if (ov < 0) ov += G;
+    const int Gi = (int)G, nvi = (int)nv;
+    const int q = t / nvi;
+    const int iu = (int)min_iu + q, iv = (int)min_iv + (t - q * nvi);
+    int ou = (Gi / 2 - S / 2 + iu * eff) % Gi;
+    int ov = (Gi / 2 - S / 2 + iv * eff) % Gi;
+    if (ou < 0) ou += Gi;
+    if (ov < 0) ov += Gi;
     int64_t gv = ov + b;                  // b < S <= G
     if (gv >= G) gv -= G;
     Cx<T> x[kCutRows];
@@ -709,6 +713,108 @@ __global__ void k_gather_grid(Cx<T>* __restrict__ grid, int64_t G64,
         acc.im += im;
     }
     grid[gi] = acc;
+}
+
+// No-wrap form of k_gather_grid, for a plane whose sub-grids all lie inside
+// the grid along both axes (host-checked; config 4 and every small test):
+// the sub-grids covering cell x are then the k = 0 image's ii in
+// [ceil((x - S + 1) / eff), floor(x / eff)], at most NC = ceil(S / eff) per
+// axis, ascending -- the same set and order as gather_candidates, so the
+// same sums. A thread takes kGatherRows consecutive rows of one column
+// (the column's candidates are found once) and issues all their slot
+// lookups, then all their sub-grid loads. The general kernel spent ~300
+// instructions per cell on the three periodic images' candidate loops
+// (SQ counters, config 4); this one ~1/4 of that.
+constexpr int kGatherRows = 4;
+
+template<int NC>
+__device__ __forceinline__ int gather_candidates_nw(int x, int S, int eff,
+        float inv_eff, int lo_idx, int n_idx, int (&off)[NC], int (&idx)[NC])
+{
+    const int i_lo = max(floor_div_small(x - S + eff, eff, inv_eff), lo_idx);
+    const int i_hi = min(floor_div_small(x, eff, inv_eff), lo_idx + n_idx - 1);
+    int nc = 0;
+#pragma unroll
+    for (int k = 0; k < NC; ++k)
+    {
+        const int ii = i_lo + k;
+        off[k] = x - ii * eff;
+        idx[k] = ii - lo_idx;
+        if (ii <= i_hi) nc = k + 1;
+    }
+    return nc;
+}
+
+template<typename T, int NC>
+__global__ void k_gather_grid_nw(Cx<T>* __restrict__ grid, int G,
+        const Cx<T>* __restrict__ stack, int S,
+        const int* __restrict__ slot_of, int nu, int nv, int min_iu,
+        int min_iv, int eff, T factor, int accumulate)
+{
+#pragma clang fp contract(off)
+    const int gv = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int gu0 = (int)blockIdx.y * kGatherRows;
+    if (gv >= G) return;
+    const float inv_eff = 1.0f / (float)eff;
+    int vb[NC], vv[NC];
+    const int nvc = gather_candidates_nw(gv - G / 2 + S / 2, S, eff, inv_eff,
+            min_iv, nv, vb, vv);
+    constexpr int kC = NC * NC;
+    const int64_t SS = (int64_t)S * S;
+    int ua[kGatherRows][NC];
+    int slot[kGatherRows][kC];
+#pragma unroll
+    for (int r = 0; r < kGatherRows; ++r)
+    {
+        int uu[NC];
+        const int gu = min(gu0 + r, G - 1);
+        const int nuc = gather_candidates_nw(gu - G / 2 + S / 2, S, eff,
+                inv_eff, min_iu, nu, ua[r], uu);
+#pragma unroll
+        for (int c = 0; c < kC; ++c)
+        {
+            const int cu = c / NC, cv = c % NC;
+            slot[r][c] = (cu < nuc && cv < nvc && gu0 + r < G) ?
+                    slot_of[uu[cu] * nv + vv[cv]] : -1;
+        }
+    }
+    Cx<T> x[kGatherRows][kC];
+#pragma unroll
+    for (int r = 0; r < kGatherRows; ++r)
+#pragma unroll
+        for (int c = 0; c < kC; ++c)
+        {
+            const int cu = c / NC, cv = c % NC;
+            x[r][c] = (slot[r][c] >= 0) ?
+                    stack[slot[r][c] * SS + ua[r][cu] * S + vb[cv]] :
+                    cx<T>(0, 0);
+        }
+#pragma unroll
+    for (int r = 0; r < kGatherRows; ++r)
+    {
+        const int gu = gu0 + r;
+        if (gu >= G) break;
+        const int64_t gi = (int64_t)gu * G + gv;
+        Cx<T> acc = accumulate ? grid[gi] : cx<T>(0, 0);
+        const bool neg_g = ((gu + gv) & 1) != 0;
+#pragma unroll
+        for (int c = 0; c < kC; ++c)
+        {
+            if (slot[r][c] < 0) continue;
+            const int cu = c / NC, cv = c % NC;
+            const bool neg = ((ua[r][cu] + vb[cv]) & 1) != 0;
+            T re = (neg ? -x[r][c].re : x[r][c].re) * factor;
+            T im = (neg ? -x[r][c].im : x[r][c].im) * factor;
+            if (neg_g)
+            {
+                re = -re;
+                im = -im;
+            }
+            acc.re += re;
+            acc.im += im;
+        }
+        grid[gi] = acc;
+    }
 }
 
 // Image-side kernels: kImgRows grid rows per thread (blockIdx.y), all rows'
@@ -2449,6 +2555,16 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
             return (int)(((g.S + g.eff - 1) / g.eff) * wraps);
         };
         const int ncand = std::max(axis_cand(g.nu), axis_cand(g.nv));
+        // No-wrap gather when every sub-grid of both axes lies inside the
+        // grid (k_gather_grid_nw).
+        auto inside = [&](int64_t min_i, int64_t n_idx) {
+            const int64_t first = G / 2 - g.S / 2 + min_i * g.eff;
+            const int64_t last = first + (n_idx - 1) * g.eff + g.S - 1;
+            return first >= 0 && last <= G - 1;
+        };
+        const int nc_nw = (int)((g.S + g.eff - 1) / g.eff);
+        const bool nowrap = inside(g.min_iu, g.nu) && inside(g.min_iv, g.nv)
+                && nc_nw <= 3 && G < (1 << 30);
         // The plane's last group with the fused f32 plane FFT: the image
         // update runs inside the FFT's last column pass (es_fft_wstack.h).
         // (A gather fused into the row pass measured 10.3 ms per plane at
@@ -2459,7 +2575,19 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                 sizeof(T) == 4) ? plane_fft_twiddles(G, false, status) :
                 nullptr;
         if (*status) break;
-        if (ncand <= 3)
+        const dim3 gnw(blocks_of(G), (unsigned)((G + kGatherRows - 1) /
+                kGatherRows));
+        if (nowrap && nc_nw <= 2)
+            k_gather_grid_nw<T, 2><<<gnw, 256>>>(d_grid, (int)G, d_stack,
+                    g.S, d_slot_of + gi * g.ntask, (int)g.nu, (int)g.nv,
+                    (int)g.min_iu, (int)g.min_iv, g.eff, factor,
+                    gr.first_of_plane ? 0 : 1);
+        else if (nowrap)
+            k_gather_grid_nw<T, 3><<<gnw, 256>>>(d_grid, (int)G, d_stack,
+                    g.S, d_slot_of + gi * g.ntask, (int)g.nu, (int)g.nv,
+                    (int)g.min_iu, (int)g.min_iv, g.eff, factor,
+                    gr.first_of_plane ? 0 : 1);
+        else if (ncand <= 3)
             k_gather_grid<T, 3><<<dim3(blocks_of(G), (unsigned)G), 256>>>(
                     d_grid, G, d_stack, g.S, d_slot_of + gi * g.ntask, g.nu,
                     g.nv, g.min_iu, g.min_iv, g.eff, factor,
