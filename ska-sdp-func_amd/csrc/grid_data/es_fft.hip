@@ -14,6 +14,7 @@
 // contiguous per row access: 256 B at L = 128, 512 B at L = 64), LDS index
 // e * B + column.
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <type_traits>
 #include <utility>
@@ -1521,14 +1522,14 @@ k_cols_b_wstack_image(const float2* __restrict__ grid, void* image_ptr,
         F::load_input(v, [&](int e) {
             return gb.load(vo, so + e * (uint32_t)G * 8u);
         });
-        // The image values and correction scales of this thread's outputs,
-        // loaded ahead of the transform (these passes are latency-bound).
+        // The image value and correction scale of an output are read in the
+        // epilogue, not ahead of the transform: holding all 16 across it
+        // took the kernel to 181 VGPRs (2 waves per SIMD) and 2.67 ms per
+        // 16384^2 plane, against 112 VGPRs and 1.68 ms this way.
         const int pm = col - G / 2;
         R prev_re[F::EPT], prev_im[kCx ? F::EPT : 1];
         float sc[F::EPT];
-#pragma unroll
-        for (int i = 0; i < F::EPT; ++i)
-        {
+        auto pre = [&](int i) {
             const int64_t gu = k2 + (int64_t)N2 * F::out_index(pq, i);
             const int64_t idx = gu * G + col;
             prev_re[i] = img[kCx ? 2 * idx : idx];
@@ -1536,9 +1537,10 @@ k_cols_b_wstack_image(const float2* __restrict__ grid, void* image_ptr,
             const int pl = (int)(gu - G / 2);
             sc[i] = sdp_wt::corr_inside(pl, pm, cp) ?
                     (float)sdp_wt::corr_scale(pl, pm, kGridKind, cp) : 1.0f;
-        }
+        };
         f.transform(v, pq, lds, ColIdx<B>{cq});
         F::store_output(v, [&](int e, int i, float2 x) {
+            pre(i);
             const int64_t gu = k2 + (int64_t)N2 * (pq + e);
             float re = x.x, im = x.y;
             if ((gu + col) & 1)
