@@ -14,6 +14,7 @@
 // contiguous per row access: 256 B at L = 128, 512 B at L = 64), LDS index
 // e * B + column.
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <cmath>
 #include <type_traits>
@@ -1983,6 +1984,136 @@ int wstack_grid_image(float2* grid, const sdp_wt::AnyView& image, float norm,
     return st;
 }
 
+// Sub-grid transforms of the w-towers imager --------------------------------
+//
+// Batched S x S complex-float 2-D FFTs (S = 128 or 256), unnormalised, in
+// place in a sub-grid stack [slots][S][S] (sdp_grid_wstack_wtower.hip; the
+// reference runs one 2-D FFT per sub-grid, sdp_grid_wstack_wtower.cpp:
+// 686-711 via sdp_gridder_wtower_uvw.cpp). Two HBM passes instead of
+// rocFFT's batched plan (whose column kernel ran at ~3.5 TB/s):
+//  columns: length-S transforms of B = 256 / (S / 16) adjacent columns per
+//           workgroup (ColFft, LDS e * B + column); in degridding the input
+//           comes straight from the FFT'd w-stack plane (the sub-grid cut-out
+//           of utils.cpp:603-649 with its checkerboard), which removes the
+//           separate cut-out pass and its sub-grid-sized write and re-read;
+//  rows   : B rows per workgroup, S / 16 consecutive lanes per row (each
+//           load / store instruction moves whole 128-byte row segments),
+//           LDS rows padded as RowIdx.
+template<int S>
+struct SubRowIdx
+{
+    static constexpr int kPitch = S + S / 16 + 8;
+    int c;
+    __device__ __forceinline__ int base(int b) const
+    {
+        return c * kPitch + b + (b >> 4);
+    }
+    static constexpr int off(int e) { return e + (e >> 4); }
+};
+
+template<int S, int SIGN, bool CUT>
+__global__ void __launch_bounds__(256) k_sub_cols(float2* __restrict__ sub,
+        const float2* __restrict__ W, SubgridCut cut)
+{
+    using F = ColFft<S, SIGN>;
+    constexpr int B = ColPlan<S>::B, NCB = S / B;
+    extern __shared__ float2 lds[];
+    const int c = threadIdx.x % B, p = threadIdx.x / B;
+    F f;
+    f.init(p, W, S);
+    const int64_t slot = blockIdx.x / NCB;
+    const int col = (int)(blockIdx.x % NCB) * B + c;
+    float2* s = sub + slot * S * S;
+    float2 v[F::EPT];
+    if constexpr (CUT)
+    {
+        // The slot's sub-grid origin in the plane grid (k_cut_out); G even,
+        // so the checkerboard sign (gu + gv + a + b) & 1 of every element
+        // is (ou + ov) & 1. Rows of the plane FFT are stored permuted.
+        const int G = cut.G;
+        const int t = cut.task[slot];
+        const int q = t / cut.nv;
+        const int iu = cut.min_iu + q, iv = cut.min_iv + (t - q * cut.nv);
+        int ou = (G / 2 - S / 2 + iu * cut.eff) % G;
+        int ov = (G / 2 - S / 2 + iv * cut.eff) % G;
+        if (ou < 0) ou += G;
+        if (ov < 0) ov += G;
+        int gv = ov + col;
+        if (gv >= G) gv -= G;
+        const float sg = ((ou + ov) & 1) ? -1.0f : 1.0f;
+        const int sh = cut.perm_shift;
+        const unsigned n2m = sh >= 0 ? (1u << sh) - 1u : 0u;
+        const unsigned n1 = sh >= 0 ? (unsigned)G >> sh : 0u;
+        F::load_input(v, [&](int e) {
+            int gu = ou + p + e;
+            if (gu >= G) gu -= G;
+            const unsigned r = sh >= 0 ? ((unsigned)gu & n2m) * n1 +
+                    ((unsigned)gu >> sh) : (unsigned)gu;
+            const float2 x = cut.grid[(size_t)r * G + gv];
+            return make_float2(sg * x.x, sg * x.y);
+        });
+    }
+    else
+    {
+        F::load_input(v, [&](int e) { return s[(p + e) * S + col]; });
+    }
+    f.transform(v, p, lds, ColIdx<B>{c});
+    F::store_output(v, [&](int e, int, float2 x) { s[(p + e) * S + col] = x; });
+}
+
+template<int S, int SIGN>
+__global__ void __launch_bounds__(256) k_sub_rows(float2* __restrict__ sub,
+        const float2* __restrict__ W)
+{
+    using F = ColFft<S, SIGN>;
+    constexpr int P = ColPlan<S>::P, B = ColPlan<S>::B;
+    extern __shared__ float2 lds[];
+    const int p = threadIdx.x % P, c = threadIdx.x / P;
+    F f;
+    f.init(p, W, S);
+    float2* r = sub + ((int64_t)blockIdx.x * B + c) * S;
+    float2 v[F::EPT];
+    F::load_input(v, [&](int e) { return r[p + e]; });
+    f.transform(v, p, lds, SubRowIdx<S>{c});
+    F::store_output(v, [&](int e, int, float2 x) { r[p + e] = x; });
+}
+
+template<int S>
+int subgrid_fft_s(float2* sub, int64_t slots, bool forward, const float2* W,
+        const SubgridCut* cut, hipStream_t stream)
+{
+    constexpr int B = ColPlan<S>::B;
+    sdp_Error st = SDP_SUCCESS;
+    if (slots <= 0) return st;
+    const size_t rl = (size_t)B * SubRowIdx<S>::kPitch * sizeof(float2);
+    // One workgroup per column block / row block (a persistent form with
+    // 4 or 8 workgroups per CU measured the same at config 4).
+    const unsigned ncol = (unsigned)(slots * (S / B));
+    const unsigned nrow = ncol;
+    if (forward)
+    {
+        k_sub_cols<S, -1, false><<<ncol, 256, kColLdsBytes, stream>>>(sub, W,
+                SubgridCut{});
+        SDP_HIP_CHECK_LAUNCH(&st);
+        if (st) return st;
+        k_sub_rows<S, -1><<<nrow, 256, rl, stream>>>(sub, W);
+    }
+    else
+    {
+        if (cut)
+            k_sub_cols<S, 1, true><<<ncol, 256, kColLdsBytes, stream>>>(sub,
+                    W, *cut);
+        else
+            k_sub_cols<S, 1, false><<<ncol, 256, kColLdsBytes, stream>>>(sub,
+                    W, SubgridCut{});
+        SDP_HIP_CHECK_LAUNCH(&st);
+        if (st) return st;
+        k_sub_rows<S, 1><<<nrow, 256, rl, stream>>>(sub, W);
+    }
+    SDP_HIP_CHECK_LAUNCH(&st);
+    return st;
+}
+
 // Dispatch on G = N1 * N2 (N2 = N1 or 2 * N1).
 #define SDP_ES_FFT_DISPATCH(G, CALL) \
     switch (G) \
@@ -2145,6 +2276,28 @@ int fft2d_wstack_grid_image(float* grid, int grid_size, const FftTwiddles& tw,
     const float2* W = (const float2*)tw.table;
     SDP_ES_FFT_DISPATCH(grid_size, (wstack_grid_image<N1, N2>((float2*)grid,
             image, norm, cp, W, stream)))
+}
+
+bool subgrid_fft_supported(int subgrid_size)
+{
+    return subgrid_size == 128 || subgrid_size == 256;
+}
+
+int subgrid_fft2d(float* sub, int subgrid_size, int64_t slots, bool forward,
+        const FftTwiddles& tw, const SubgridCut* cut, hipStream_t stream)
+{
+    if (tw.G != subgrid_size || slots * subgrid_size > INT32_MAX ||
+            (cut && (cut->G % 2 != 0 || cut->G < subgrid_size)))
+        return SDP_ERR_INVALID_ARGUMENT;
+    const float2* W = (const float2*)tw.table;
+    switch (subgrid_size)
+    {
+    case 128: return subgrid_fft_s<128>((float2*)sub, slots, forward, W, cut,
+            stream);
+    case 256: return subgrid_fft_s<256>((float2*)sub, slots, forward, W, cut,
+            stream);
+    default: return SDP_ERR_INVALID_ARGUMENT;
+    }
 }
 
 int fft_perm_n2(int grid_size)

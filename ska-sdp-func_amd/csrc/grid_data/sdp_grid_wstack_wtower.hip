@@ -1907,6 +1907,25 @@ const sdp_es::FftTwiddles* plane_fft_twiddles(int64_t G, bool dbl,
     return &(cache[key] = tw);
 }
 
+// Twiddles of the batched sub-grid FFT (es_fft_wstack.h subgrid_fft2d):
+// complex-float sub-grids of S = 128 or 256 (rocFFT otherwise).
+const sdp_es::FftTwiddles* subgrid_fft_twiddles(int S, bool dbl,
+        sdp_Error* status)
+{
+    if (dbl || !sdp_es::subgrid_fft_supported(S)) return nullptr;
+    static std::map<std::pair<int, int>, sdp_es::FftTwiddles> cache;
+    const auto key = std::make_pair(current_device(), S);
+    auto it = cache.find(key);
+    if (it != cache.end()) return &it->second;
+    sdp_es::FftTwiddles tw;
+    if (sdp_es::fft_twiddles_create(S, &tw) != 0)
+    {
+        *status = SDP_ERR_RUNTIME;
+        return nullptr;
+    }
+    return &(cache[key] = tw);
+}
+
 sdp_GridderWtowerUVW* cached_kernel(int image_size, int S, double theta,
         double w_step, double hu, double hv, int support, int os,
         int w_support, int wos, sdp_Error* status)
@@ -2489,7 +2508,18 @@ void grid_all_impl(sdp_GridderWtowerUVW* k, Geo g, const Cx<T>* d_vis,
                             (const Cx<float>*)d_vis);
                 SDP_HIP_CHECK_LAUNCH(status);
                 tower_timing().stop();
-                sdp_fft::exec_2d(sp, d_stack, true, 0, status);
+                const sdp_es::FftTwiddles* stw = subgrid_fft_twiddles(g.S,
+                        false, status);
+                if (stw)
+                {
+                    const int e = sdp_es::subgrid_fft2d((float*)d_stack, g.S,
+                            gr.slots, true, *stw, nullptr, 0);
+                    if (e) *status = (sdp_Error)e;
+                }
+                else
+                {
+                    sdp_fft::exec_2d(sp, d_stack, true, 0, status);
+                }
             }
             tm.layers += (gr.last_p - gr.first_p + ws_n) * gr.slots;
         }
@@ -2800,14 +2830,37 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
         TowerParams p = tower_params(k, g, gr, b);
         const int64_t n_el = gr.slots * layer;
         const int64_t ls = p.layer_stride;
+        // Fused f32 towers with S = 128 / 256 (even G): the cut-out is read
+        // by the first pass of the batched sub-grid FFT (es_fft_wstack.h);
+        // otherwise k_cut_out + rocFFT.
+        const sdp_es::FftTwiddles* stw = (g.fused && G % 2 == 0 &&
+                G < (1 << 30) && sizeof(T) == 4) ?
+                subgrid_fft_twiddles(g.S, false, status) : nullptr;
+        if (*status) break;
+        if (stw)
+        {
+            sdp_es::SubgridCut cut;
+            cut.grid = (const float2*)(const void*)d_grid;
+            cut.G = (int)G;
+            cut.task = p.task;
+            cut.nv = (int)g.nv;
+            cut.min_iu = (int)g.min_iu;
+            cut.min_iv = (int)g.min_iv;
+            cut.eff = g.eff;
+            cut.perm_shift = perm_n2 ? __builtin_ctz((unsigned)perm_n2) : -1;
+            const int e = sdp_es::subgrid_fft2d((float*)d_wimg, g.S, gr.slots,
+                    false, *stw, &cut, 0);
+            if (e) *status = (sdp_Error)e;
+        }
+        else
         {
             const int nbx = (g.S + 255) / 256;
             k_cut_out<T><<<dim3((unsigned)(gr.slots_alloc * nbx),
                     (unsigned)((g.S + kCutRows - 1) / kCutRows)), 256>>>(d_grid, G, d_wimg, g.S, layer,
                     p.task, g.nv, g.min_iu, g.min_iv, g.eff, gr.slots, nbx,
                     perm_n2);
+            sdp_fft::exec_2d(sp, d_wimg, false, 0, status);
         }
-        sdp_fft::exec_2d(sp, d_wimg, false, 0, status);
         const int64_t first = gr.first_p + g.P0 - p.off_w;
         const int64_t last = gr.last_p + g.P0 - p.off_w;
         if (g.fused)

@@ -287,6 +287,36 @@ def test_fused_towers_match_double_precision(device, degrid):
         _close(im32.cpu().numpy(), im64.cpu().numpy(), 5e-5, border=N // 4)
 
 
+@pytest.mark.parametrize("degrid", [False, True])
+def test_fused_towers_dense_vs_oracle(device, degrid):
+    """The complex-float product path (fused tower kernels) against the
+    oracle on a case dense enough that a sub-grid's per-layer visibility
+    windows overflow the kernels' LDS rings (restaging, multi-piece
+    windows, partial-sum flushes). The oracle needs about a minute per
+    direction here, so its outputs are golden vectors made by
+    tests/golden/make_wtower_dense.py (inputs regenerated from the same
+    seeds)."""
+    import os
+    import torch
+    import ska_sdp_func.grid_data as g
+    from golden.make_wtower_dense import N, inputs
+    gold = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                "golden", "wtower_dense.npz"))
+    c, vis, img, a = inputs()
+    dev = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(device)
+    if degrid:
+        out = torch.zeros(vis.shape, dtype=torch.complex64, device=device)
+        g.wstack_wtower_degrid_all(dev(img.astype(np.float32)), a[0], a[1],
+                                   dev(c["uvw"]), *a[3:], 0, out)
+        _close(out.cpu().numpy(), gold["degrid"], 1e-5)
+    else:
+        out = torch.zeros((N, N), dtype=torch.float32, device=device)
+        g.wstack_wtower_grid_all(dev(vis.astype(np.complex64)), a[0], a[1],
+                                 dev(c["uvw"]), *a[3:], 0, out)
+        b = N // 4
+        _close(out.cpu().numpy()[b:-b, b:-b], gold["grid_interior"], 5e-5)
+
+
 @pytest.mark.parametrize("uv_frac", [0.75, 1.3])
 def test_uv_extent_wider_than_grid(device, uv_frac):
     """Sub-grids past the grid edge wrap onto it (subgrid_add / cut_out use
