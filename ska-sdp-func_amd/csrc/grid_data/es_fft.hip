@@ -1569,6 +1569,81 @@ k_cols_b_wstack_image(const float2* __restrict__ grid, void* image_ptr,
     }
 }
 
+// Degridding a w-stack plane starts with grid = checker(degrid_correct(
+// (float)image)) and its forward FFT (k_image_to_grid + rows + four-step
+// columns; ref sdp_grid_wstack_wtower.cpp:363-375). A 2-D transform may
+// take its axes in either order, so here the columns go first and column
+// pass A reads the image itself: the grid is neither written by a prologue
+// pass nor re-read by the row pass (2 GiB each at G = 16384). Column pass B
+// (k_cols_b_block) and the row pass (k_rows_image over whole rows) follow;
+// the result has the stored-row permutation of fft2d_inplace_permuted.
+//
+// Column pass A (forward) with the image prologue: for u1 = blockIdx.x,
+// length-N2 FFTs over rows u1 + N1 * n2 of the prologue's values, in the
+// order and precision of k_image_to_grid (the image value rounded to
+// float, correct_scaled_f32 with the kind-2 scale, checkerboard), times
+// W^(u1 k2), into rows u1 + N1 * k2. IK: the image kind (AnyView).
+#ifndef SDP_WSA_WAVES
+#define SDP_WSA_WAVES 4
+#endif
+template<int N1, int N2, int IK>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SDP_WSA_WAVES)))
+k_cols_a_wstack_image(float2* __restrict__ grid, const void* image_ptr,
+        sdp_wt::CorrParams cp, const float2* __restrict__ W)
+{
+#pragma clang fp contract(off)
+    constexpr int G = N1 * N2, B = ColPlan<N2>::B;
+    constexpr int kGridKind = 2;                  // complex float grid
+    using F = ColFft<N2, -1>;
+    using R = typename std::conditional<(IK == 1 || IK == 3), double,
+            float>::type;
+    constexpr bool kCx = IK >= 2;
+    extern __shared__ float2 lds[];
+    const int c = threadIdx.x % B, p = threadIdx.x / B;
+    const int u1 = blockIdx.x;
+    const Buf gb(grid, grid_bytes(G, 0));
+    const R* img = (const R*)image_ptr;
+    F f;
+    f.init(p, W, G);
+    float2 fs[F::EPT];
+#pragma unroll
+    for (int i = 0; i < F::EPT; ++i)
+        fs[i] = F::twiddle(W, u1 * F::out_index(p, i));
+    const int ncb = G / B;
+    const uint32_t so = (uint32_t)u1 * G * 8u;
+    constexpr uint32_t kStep = (uint32_t)N1 * G * 8u;   // one n2 / k2 step
+    for (int cb = blockIdx.y; cb < ncb; cb += gridDim.y)
+    {
+        const int pq = opaque(p), cq = opaque(c);
+        const int col = cb * B + cq;
+        const int pm = col - G / 2;
+        const uint32_t vo = ((uint32_t)pq * N1 * G + col) * 8u;
+        float2 v[F::EPT];
+        F::load_input(v, [&](int e) {
+            const int gu = u1 + N1 * (pq + e);
+            const int64_t idx = (int64_t)gu * G + col;
+            const float re = (float)img[kCx ? 2 * idx : idx];
+            const float im = kCx ? (float)img[2 * idx + 1] : 0.0f;
+            sdp_wt::Cx<double> z = sdp_wt::cx<double>(re, im);
+            const int pl = gu - G / 2;
+            if (sdp_wt::corr_inside(pl, pm, cp))
+                z = sdp_wt::correct_scaled_f32(z, pl, pm, cp,
+                        (float)sdp_wt::corr_scale(pl, pm, kGridKind, cp));
+            float zr = (float)z.re, zi = (float)z.im;
+            if ((gu + col) & 1)
+            {
+                zr = -zr;
+                zi = -zi;
+            }
+            return make_float2(zr, zi);
+        });
+        f.transform(v, pq, lds, ColIdx<B>{cq});
+        F::store_output(v, [&](int e, int i, float2 x) {
+            gb.store(cmul(x, fs[i]), vo, so + e * kStep);
+        });
+    }
+}
+
 // Launch helpers --------------------------------------------------------------
 
 int num_cus()
@@ -2114,6 +2189,42 @@ int subgrid_fft_s(float2* sub, int64_t slots, bool forward, const float2* W,
     return st;
 }
 
+// Forward FFT of a w-stack plane from its image (degridding prologue):
+// columns (image prologue) first, then rows.
+template<int N1, int N2>
+int wstack_image_to_grid(float2* grid, const sdp_wt::AnyView& image,
+        const sdp_wt::CorrParams& cp, const float2* W, hipStream_t stream)
+{
+    constexpr int G = N1 * N2;
+    sdp_Error st = SDP_SUCCESS;
+#define SDP_WS_COLA(IK) \
+    k_cols_a_wstack_image<N1, N2, IK><<<col_grid<k_cols_a_wstack_image<N1, \
+            N2, IK>>(N1, G, ColPlan<N2>::B), 256, kColLdsBytes, stream>>>( \
+            grid, image.ptr, cp, W)
+    switch (image.kind)
+    {
+    case 0: SDP_WS_COLA(0); break;
+    case 1: SDP_WS_COLA(1); break;
+    case 2: SDP_WS_COLA(2); break;
+    case 3: SDP_WS_COLA(3); break;
+    default: return SDP_ERR_INVALID_ARGUMENT;
+    }
+#undef SDP_WS_COLA
+    SDP_HIP_CHECK_LAUNCH(&st);
+    if (st) return st;
+    k_cols_b_block<N1, N2, -1><<<col_grid<k_cols_b_block<N1, N2, -1>>(N2, G,
+            ColPlan<N1>::B), 256, kColLdsBytes, stream>>>(grid, G, W);
+    SDP_HIP_CHECK_LAUNCH(&st);
+    if (st) return st;
+    const size_t lds = row_lds_bytes(G);
+    SDP_HIP_CHECK((allow_lds<k_rows_image<G>>(lds)), &st);
+    if (st) return st;
+    k_rows_image<G><<<row_blocks(G), RowPlan<G>::P, lds, stream>>>(grid, 0,
+            G, W, nullptr, 0);
+    SDP_HIP_CHECK_LAUNCH(&st);
+    return st;
+}
+
 // Dispatch on G = N1 * N2 (N2 = N1 or 2 * N1).
 #define SDP_ES_FFT_DISPATCH(G, CALL) \
     switch (G) \
@@ -2276,6 +2387,16 @@ int fft2d_wstack_grid_image(float* grid, int grid_size, const FftTwiddles& tw,
     const float2* W = (const float2*)tw.table;
     SDP_ES_FFT_DISPATCH(grid_size, (wstack_grid_image<N1, N2>((float2*)grid,
             image, norm, cp, W, stream)))
+}
+
+int fft2d_wstack_image_to_grid(float* grid, int grid_size,
+        const FftTwiddles& tw, const sdp_wt::AnyView& image,
+        const sdp_wt::CorrParams& cp, hipStream_t stream)
+{
+    if (tw.G != grid_size) return SDP_ERR_INVALID_ARGUMENT;
+    const float2* W = (const float2*)tw.table;
+    SDP_ES_FFT_DISPATCH(grid_size, (wstack_image_to_grid<N1, N2>(
+            (float2*)grid, image, cp, W, stream)))
 }
 
 bool subgrid_fft_supported(int subgrid_size)

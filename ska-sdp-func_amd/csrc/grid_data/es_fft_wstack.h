@@ -18,6 +18,15 @@ int fft2d_wstack_grid_image(float* grid, int grid_size, const FftTwiddles& tw,
         const sdp_wt::AnyView& image, float norm,
         const sdp_wt::CorrParams& cp, hipStream_t stream);
 
+// grid = FFT2(checker(degrid_correct((float)image))) for a w-stack plane
+// (cp: its correction, w_offset included), unnormalised forward transform
+// with the stored-row permutation of fft2d_inplace_permuted; the prologue
+// is read by the first column pass (no separate pass over the grid). G a
+// power of two in [1024, 16384] with tw its twiddles.
+int fft2d_wstack_image_to_grid(float* grid, int grid_size,
+        const FftTwiddles& tw, const sdp_wt::AnyView& image,
+        const sdp_wt::CorrParams& cp, hipStream_t stream);
+
 // Sub-grid cut-out read by the first pass of subgrid_fft2d (degridding):
 // element (a, b) of slot k's sub-grid is (-1)^(ou + ov) grid[row(gu)][gv]
 // with gu = (ou + a) mod G, gv = (ov + b) mod G, (ou, ov) the origin of

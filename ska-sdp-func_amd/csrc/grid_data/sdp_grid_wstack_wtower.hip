@@ -2792,12 +2792,10 @@ void degrid_all_impl(sdp_GridderWtowerUVW* k, Geo g, AnyView image,
             // workgroup per CU.)
             if (tw)
             {
-                k_image_to_grid<T><<<dim3(blocks_of(G),
-                        (unsigned)((G + kImgRows - 1) / kImgRows)), 256>>>(
-                        image, G, d_grid, cp);
-                SDP_HIP_CHECK_LAUNCH(status);
-                const int e = sdp_es::fft2d_inplace_permuted((float*)d_grid,
-                        (int)G, true, *tw, 0);
+                // Complex float: the prologue is read by the plane FFT's
+                // first (column) pass (es_fft_wstack.h).
+                const int e = sdp_es::fft2d_wstack_image_to_grid(
+                        (float*)d_grid, (int)G, *tw, image, cp, 0);
                 if (e) *status = (sdp_Error)e;
             }
             else
