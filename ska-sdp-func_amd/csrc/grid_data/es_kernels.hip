@@ -1596,7 +1596,13 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     constexpr int kStride = NTAP + 15;
     constexpr int kLead = 16;
     constexpr int kTab = kLead + CHUNK * kStride;
-    static_assert(kTab < 65536, "16-bit table indices");
+    // Visit words hold byte offsets (u | v << 16) and the visibility's byte
+    // offset, so a visit's three LDS addresses cost one packed 16-bit add,
+    // an and and a shift (round 6; with table indices they took an and, a
+    // bit-field extract, two shift-adds and a shift: tile kernel 0.439 ->
+    // 0.420 ms at config 2, 25.1 -> 24.2 ms at config 3).
+    constexpr uint32_t kPosUnit = 4, kVisUnit = 8;
+    static_assert((kTab + 128) * kPosUnit < 65536, "16-bit table offsets");
     static_assert(kLead % 4 == 0 && kStride % 4 == 0, "16-byte table rows");
     __shared__ __attribute__((aligned(16))) float s_ku[kTab];
     __shared__ __attribute__((aligned(16))) float s_kv[kTab];
@@ -1604,8 +1610,8 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     __shared__ float2 s_visx[kX][PLANES > 1 ? CHUNK + 1 : 1];
     __shared__ uint2 s_list[4][CHUNK + 4];
     // Per entry: byte 0 = row bands hit, byte 1 = column blocks hit (0 for
-    // entries past the chunk); s_pos: table index of the entry's row 0 /
-    // column 0 of the tile, + 64 (lo: u, hi: v). With CHUNK = 128 the u
+    // entries past the chunk); s_pos: table byte offset of the entry's row
+    // 0 / column 0 of the tile, + 64 taps (lo: u, hi: v). With CHUNK = 128 the u
     // half and the v half of both are written by the entry's two threads.
     __shared__ uint32_t s_info[CHUNK];
     __shared__ uint32_t s_pos[CHUNK];
@@ -1632,6 +1638,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
     const int lane = t & 63, wave = t >> 6;
     const int i = lane & 15, kq = lane >> 4;
     const int sub_r = wave * 16;
+    const uint32_t li4 = (uint32_t)(4 * i) * 0x10001u;   // (4 i, 4 i) bytes
     const int et = t & (kHalf - 1);               // this thread's entry
     const bool stage_u = CHUNK == 256 || t < 128;
     const bool stage_v = CHUNK == 256 || t >= 128;
@@ -1710,7 +1717,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 const int lo = max(u0 - tu0, 0) >> 4;
                 const int hi = min(u1 - tu0, kTile - 1) >> 4;
                 rm = on_plane ? (2u << hi) - (1u << lo) : 0u;
-                pu16 = (uint32_t)(eb + 64 - (u0 - tu0));
+                pu16 = (uint32_t)(eb + 64 - (u0 - tu0)) * kPosUnit;
             }
             if (stage_v)
             {
@@ -1719,7 +1726,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 const int lo = max(v0 - tv0, 0) >> 4;
                 const int hi = min(v1 - tv0, kTile - 1) >> 4;
                 cm = on_plane ? (2u << hi) - (1u << lo) : 0u;
-                pv16 = (uint32_t)(eb + 64 - (v0 - tv0));
+                pv16 = (uint32_t)(eb + 64 - (v0 - tv0)) * kPosUnit;
             }
         }
         lds_barrier();   // B1: previous chunk's tables and lists consumed
@@ -1783,6 +1790,24 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         lds_barrier();   // B2: entry words and tap tables complete
 
         uint2* list = s_list[wave];
+        // A visit's operands: tap rows at byte offsets w.x + (4 i, 4 i)
+        // (one packed 16-bit add; the halves do not carry into each other),
+        // the weighted visibility at byte offset w.y.
+        auto vis_at = [&](const float2* base, uint32_t off) -> float2 {
+            return *reinterpret_cast<const float2*>(
+                    reinterpret_cast<const char*>(base) + off);
+        };
+        auto visit_operands = [&](uint2 w, float& a, float& kv, float2& z) {
+            typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+            const us2 ab = __builtin_bit_cast(us2, w.x) +
+                    __builtin_bit_cast(us2, li4);
+            const uint32_t abw = __builtin_bit_cast(uint32_t, ab);
+            a = *reinterpret_cast<const float*>(
+                    reinterpret_cast<const char*>(s_ku) + (abw & 0xffffu));
+            kv = *reinterpret_cast<const float*>(
+                    reinterpret_cast<const char*>(s_kv) + (abw >> 16));
+            z = vis_at(s_vis, w.y);
+        };
         // The chunk's entry words, read once for the four column blocks.
         constexpr int kGroups = (CHUNK + 63) / 64;
         uint32_t inf[kGroups], ps[kGroups];
@@ -1798,11 +1823,11 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         for (int cblk = 0; cblk < 4; ++cblk)
         {
             // This wave's visits of sub-tile (wave, cblk), in entry order.
-            // Visit word = entry word + (sub_r - 64, cblk * 16 - 64): both
-            // halves stay non-negative for a visited sub-tile, so the one
-            // 32-bit add does not carry between them.
-            const uint32_t kadd = (uint32_t)(sub_r - 64) +
-                    ((uint32_t)(cblk * 16 - 64) << 16);
+            // Visit word = entry word + 4 (sub_r - 64, cblk * 16 - 64)
+            // bytes: both halves stay non-negative for a visited sub-tile,
+            // so the one 32-bit add does not carry between them.
+            const uint32_t kadd = (uint32_t)((sub_r - 64) * (int)kPosUnit) +
+                    ((uint32_t)((cblk * 16 - 64) * (int)kPosUnit) << 16);
             int cnt = 0;
 #pragma unroll
             for (int gi = 0; gi < kGroups; ++gi)
@@ -1811,12 +1836,12 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
                 const uint64_t m = __ballot(hit);
                 if (hit)
                     list[cnt + (int)__popcll(m & below)] = make_uint2(
-                            ps[gi] + kadd, (uint32_t)(gi * 64 + lane));
+                            ps[gi] + kadd, (uint32_t)(gi * 64 + lane) * kVisUnit);
                 cnt += (int)__popcll(m);
             }
             const int cnt4 = (cnt + 3) & ~3;
             if (lane < cnt4 - cnt)     // zero visit (zero taps, zero value)
-                list[cnt + lane] = make_uint2(0u, (uint32_t)CHUNK);
+                list[cnt + lane] = make_uint2(0u, (uint32_t)CHUNK * kVisUnit);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
@@ -1834,9 +1859,9 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
             for (int g = n16; g < n4; g += 4)
             {
                 const uint2 w = list[g + kq];
-                const float a = s_ku[(w.x & 0xffffu) + i];
-                const float kv = s_kv[(w.x >> 16) + i];
-                const float2 z = s_vis[w.y];
+                float a, kv;
+                float2 z;
+                visit_operands(w, a, kv, z);
                 const float2 bb = make_float2(kv * z.x, kv * z.y);
                 re = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.x, re, 0, 0, 0);
                 im = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bb.y, im, 0, 0, 0);
@@ -1844,7 +1869,7 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
 #pragma unroll
                     for (int x = 0; x < kX; ++x)
                     {
-                        const float2 z2 = s_visx[x][w.y];
+                        const float2 z2 = vis_at(s_visx[x], w.y);
                         rex[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a,
                                 kv * z2.x, rex[x], 0, 0, 0);
                         imx[x] = __builtin_amdgcn_mfma_f32_16x16x4f32(a,
@@ -1862,15 +1887,19 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
 #pragma unroll
                 for (int s2 = 0; s2 < 4; ++s2)
                 {
-                    a[s2] = s_ku[(w[s2].x & 0xffffu) + i];
-                    const float kv = s_kv[(w[s2].x >> 16) + i];
-                    const float2 z = s_vis[w[s2].y];
-                    bb[s2] = make_float2(kv * z.x, kv * z.y);
+                    float kv;
+                    float2 z;
+                    visit_operands(w[s2], a[s2], kv, z);
+                    {
+                        using f2v = __attribute__((ext_vector_type(2))) float;
+                        const f2v pb = f2v{kv, kv} * f2v{z.x, z.y};
+                        bb[s2] = make_float2(pb.x, pb.y);
+                    }
                     if constexpr (PLANES > 1)
 #pragma unroll
                         for (int x = 0; x < kX; ++x)
                         {
-                            const float2 z2 = s_visx[x][w[s2].y];
+                            const float2 z2 = vis_at(s_visx[x], w[s2].y);
                             bbx[x][s2] = make_float2(kv * z2.x, kv * z2.y);
                         }
                 }
