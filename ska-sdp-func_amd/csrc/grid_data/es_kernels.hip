@@ -1810,15 +1810,16 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
         };
         // The chunk's entry words, read once for the four column blocks.
         constexpr int kGroups = (CHUNK + 63) / 64;
-        uint32_t inf[kGroups], ps[kGroups];
+        // cbm: the column blocks an entry hits in this wave's row band.
+        uint32_t cbm[kGroups], ps[kGroups];
 #pragma unroll
         for (int gi = 0; gi < kGroups; ++gi)
         {
             const bool in = CHUNK % 64 == 0 || gi * 64 + lane < CHUNK;
-            inf[gi] = in ? s_info[gi * 64 + lane] : 0u;
+            const uint32_t inf = in ? s_info[gi * 64 + lane] : 0u;
+            cbm[gi] = ((inf >> wave) & 1u) ? (inf >> 8) & 0xFu : 0u;
             ps[gi] = in ? s_pos[gi * 64 + lane] : 0u;
         }
-        const uint64_t below = (1ull << lane) - 1ull;
 #pragma unroll
         for (int cblk = 0; cblk < 4; ++cblk)
         {
@@ -1832,11 +1833,14 @@ __global__ __launch_bounds__(256) void k_scatter_tab(EsParams<float> p,
 #pragma unroll
             for (int gi = 0; gi < kGroups; ++gi)
             {
-                const bool hit = (inf[gi] >> wave) & (inf[gi] >> (8 + cblk)) & 1u;
+                const bool hit = (cbm[gi] & (1u << cblk)) != 0u;
                 const uint64_t m = __ballot(hit);
+                // Slot cnt + (hits in lanes below): one mbcnt pair.
                 if (hit)
-                    list[cnt + (int)__popcll(m & below)] = make_uint2(
-                            ps[gi] + kadd, (uint32_t)(gi * 64 + lane) * kVisUnit);
+                    list[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                            __builtin_amdgcn_mbcnt_lo((uint32_t)m,
+                            (uint32_t)cnt))] = make_uint2(ps[gi] + kadd,
+                            (uint32_t)(gi * 64 + lane) * kVisUnit);
                 cnt += (int)__popcll(m);
             }
             const int cnt4 = (cnt + 3) & ~3;
