@@ -24,12 +24,15 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ska-sdp-func_amd"))
 sys.path.insert(0, ROOT)
 
 C_0 = 299792458.0
 F32_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E (MI355X_MICROARCH.md)
 KW = dict(support=8, oversampling=16384, w_support=8, w_oversampling=16384)
 # Image-side cost of one w-stack plane (plane FFT, cut-out / update, grid
 # gather) in units of the mean plane's visibility load: ~8 ms against
@@ -174,6 +177,29 @@ def roofline(tm, kernel):
             "algorithmic_flops_per_launch": flops}
 
 
+def image_side(ms_per_call, tm, n_planes, G):
+    """Roofline of the image side of a call (everything but the tower
+    kernels: binning, sub-grid FFTs, gather / cut-out, plane FFT, image
+    update): its time is the call's minus the live-timed tower kernels',
+    per w-stack plane; its bytes per plane are SURVEY 8(d)'s 7 G^2 s_g
+    (zero + sub-grid adds + one FFT read/write + grid-correct RMW + image
+    accumulate, complex-float grid). HBM bound."""
+    if not tm or not tm["launches"] or n_planes <= 0:
+        return None
+    t_plane = (ms_per_call - tm["kernel_ms"]) / n_planes
+    if t_plane <= 0:
+        return None
+    algo = 7.0 * G * G * 8
+    achieved = algo / (t_plane * 1e-3) / 1e9
+    return {"what": "non-tower time per w-stack plane (call minus the "
+                    "event-timed tower kernels)",
+            "bound": "hbm", "ms_per_plane": round(t_plane, 3),
+            "algorithmic_bytes_per_plane": algo,
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "planes": n_planes}
+
+
 def main():
     args = parse()
     import torch
@@ -241,8 +267,13 @@ def main():
     g.wstack_wtower_enable_timing(True)
     grid_step()
     barrier()
-    roof = roofline(g.wstack_wtower_get_timing(), "k_tower_dft")
+    tm_grid = g.wstack_wtower_get_timing()
+    roof = roofline(tm_grid, "k_tower_dft")
     g.wstack_wtower_enable_timing(False)
+    # Occupied w-stack planes of this rank (one tower launch each unless a
+    # plane's sub-grids need several groups).
+    n_planes = int(((np.asarray(loads) > 0) & np.asarray(masks[rank])).sum())
+    img_side = image_side(1e3 * t_grid / args.steps, tm_grid, n_planes, N)
     if args.verbosity:
         grid_step(args.verbosity)
         barrier()
@@ -264,11 +295,14 @@ def main():
         g.wstack_wtower_degrid_plane_set(image, *common, 0, out, first,
                                          my_mask)
         barrier()
-        droof = roofline(g.wstack_wtower_get_timing(), "k_tower_idft")
+        tm_deg = g.wstack_wtower_get_timing()
+        droof = roofline(tm_deg, "k_tower_idft")
         g.wstack_wtower_enable_timing(False)
         degrid = {"mvis_s": round(total_vis * args.steps / t_deg / 1e6, 3),
                   "ms_per_step": round(1e3 * t_deg / args.steps, 2),
-                  "roofline": droof}
+                  "roofline": droof,
+                  "image_side": image_side(1e3 * t_deg / args.steps, tm_deg,
+                                           n_planes, N)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -303,6 +337,7 @@ def main():
                 "plane_balance": round(plane_balance(pcost), 4),
             },
             "roofline": roof,
+            "image_side": img_side,
             "degrid": degrid,
             "cpu_baseline": cpu,
         }
