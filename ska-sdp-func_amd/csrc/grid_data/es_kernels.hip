@@ -2312,6 +2312,14 @@ __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
         tap_range(p, rc.x, rc.y, u0, u1, v0, v1);
         if (kParts > 1 && (unsigned)(u0 - tu0 - ru_lo) >= (unsigned)ROWS)
             continue;                          // the other part's entry
+        // The visibility's current value, loaded before the taps and the
+        // contraction so that its latency overlaps them (the entry is the
+        // visibility's only one: degrid records sit in the tile of their
+        // first tap). Read at the end, its round trip and the store's
+        // completion sat in every iteration.
+        const uint64_t idx = (uint64_t)__float_as_uint(rc.w);
+        float2* vdst = reinterpret_cast<float2*>(vis + 2 * idx);
+        const float2 vold = *vdst;
         float tu[NTAP], tv[NTAP];
         axis_taps<NTAP, true>(p, rc.x, u0, u1, tu);
         axis_taps<NTAP, true>(p, rc.y, v0, v1, tv);
@@ -2382,10 +2390,8 @@ __global__ __launch_bounds__(NT) void k_gather_win(EsParams<float> p,
         // (-1)^(u0 + v0) of the checkerboard, with the w-tap; the flip
         // conjugates (kernels.cu:267-268).
         const float ks = ((u0 + v0) & 1) ? -kw : kw;
-        const uint64_t idx = (uint64_t)__float_as_uint(rc.w);
         const float flip = signbit(rc.z) ? -1.0f : 1.0f;
-        vis[2 * idx] += sr * ks;
-        vis[2 * idx + 1] += si * ks * flip;
+        *vdst = make_float2(vold.x + sr * ks, vold.y + si * ks * flip);
     }
 }
 
