@@ -66,8 +66,8 @@ __device__ __forceinline__ float es_tap_fast(float beta, float x)
 // tap, the two edge taps (d = 0, 7: the sqrt branch point makes them
 // non-polynomial) and the exact-integer ninth tap are evaluated that way,
 // and the six interior taps (smooth in delta = u0 - (pos - 4) in [0, 1))
-// as degree-10 polynomials of s = 2 delta - 1 in packed-f32 Horner form,
-// two taps per v_pk_fma_f32 (~5e-7 relative in f32, es_tap_poly_fit):
+// as degree-8 polynomials of s = 2 delta - 1 in packed-f32 Horner form,
+// two taps per v_pk_fma_f32 (~9e-8 absolute in f32, es_tap_poly_fit):
 // 3 exp/sqrt pairs per axis instead of 9.
 template<int NTAP, bool POLY>
 __device__ __forceinline__ void axis_taps(const EsParams<float>& p, float pos,
